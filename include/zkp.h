@@ -1,0 +1,165 @@
+/*
+ * zkp.h — C-ABI of the MI355X-native STARK prover (libzkp.so).
+ *
+ * Drop-in boundary for the reference's proving path: winterfell 0.12's
+ * `Prover::prove(&self, trace) -> Result<Proof, ProverError>` as driven by the
+ * project's plug-ins
+ *   /root/reference/src/aggregation/prover.rs:194-248  (GlobalUpdateProver)
+ *   /root/reference/src/training/prover.rs:221-300     (TrainingUpdateProver)
+ * and called from /root/reference/src/main.rs:228,424,468.
+ * The `Default*` engine components those plug-ins select (DefaultTraceLde,
+ * DefaultConstraintEvaluator, DefaultConstraintCommitment, Blake3_256,
+ * MerkleTree, DefaultRandomCoin, FRI) are what this library replaces.
+ *
+ * Conventions
+ *  - Field: winter-math f128 (p = 2^128 - 45*2^40 + 1). A felt is 16 bytes,
+ *    canonical, little-endian: identical to `BaseElement` memory and to
+ *    `Serializable` bytes (reference: src/aggregation/air.rs:10).
+ *  - Traces are column-major (`ColMatrix`, what `TraceTable::init(transpose(rows))`
+ *    produces: src/aggregation/prover.rs:157-160, src/helper.rs:197-211):
+ *    element (row r, column c) lives at cols[c * n + r].
+ *  - Inputs are borrowed for the call; outputs are callee-allocated and
+ *    released with zkp_free(). No exceptions or aborts cross the ABI: every
+ *    entry point returns a zkp_status.
+ *  - Calls on one zkp_ctx are synchronous and must not overlap (the
+ *    reference's `prove(&self)` is blocking). Use one ctx per thread.
+ *  - There is no CPU fallback: if no gfx950 device is present every compute
+ *    entry point fails with ZKP_ERR_DEVICE.
+ */
+#ifndef ZKP_H
+#define ZKP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct zkp_felt {
+  uint64_t lo;
+  uint64_t hi;
+} zkp_felt;
+
+/* AIRs are identified by id because the device cannot run Rust
+ * `Air::evaluate_transition`; parameters come from `pub_inputs.to_elements()`.
+ *  MIMC          : builder-defined MiMC AIR (the reference has none, F2).
+ *                  width 1, pub = [x0, x_last].
+ *  GLOBAL_UPDATE : GlobalUpdateAir, src/aggregation/air.rs:89-151. width 120,
+ *                  pub = GlobalUpdateInputs::to_elements() (123 felts, air.rs:57-81).
+ *  TRAINING_UPDATE: reserved; returns ZKP_ERR_UNSUPPORTED_AIR. */
+typedef enum zkp_air_id {
+  ZKP_AIR_MIMC = 1,
+  ZKP_AIR_GLOBAL_UPDATE = 2,
+  ZKP_AIR_TRAINING_UPDATE = 3
+} zkp_air_id;
+
+/* winterfell `BatchingMethod`. */
+enum { ZKP_BATCHING_LINEAR = 0, ZKP_BATCHING_ALGEBRAIC = 1, ZKP_BATCHING_HORNER = 2 };
+/* winterfell `FieldExtension` (only None is supported, as in the reference). */
+enum { ZKP_FIELD_EXTENSION_NONE = 1 };
+
+/* winterfell `ProofOptions::new(num_queries, blowup_factor, grinding_factor,
+ * field_extension, fri_folding_factor, fri_remainder_max_degree,
+ * batching_constraints, batching_deep)`; the reference's set is
+ * (40, 16, 21, None, 16, 7, Algebraic, Algebraic) at src/main.rs:98-107. */
+typedef struct zkp_proof_options {
+  uint32_t num_queries;
+  uint32_t blowup_factor;
+  uint32_t grinding_factor;
+  uint32_t field_extension;
+  uint32_t fri_folding_factor;
+  uint32_t fri_remainder_max_degree;
+  uint32_t batching_constraints;
+  uint32_t batching_deep;
+} zkp_proof_options;
+
+/* Status codes; non-zero values map onto winterfell `ProverError` classes. */
+typedef enum zkp_status {
+  ZKP_OK = 0,
+  ZKP_ERR_INVALID_OPTIONS = 1,
+  ZKP_ERR_UNSUPPORTED_FIELD_EXTENSION = 2,
+  ZKP_ERR_TRACE_SHAPE = 3,   /* n < 8, n not a power of two, width 0 or > 255, n*blowup too big */
+  ZKP_ERR_PUB_INPUTS = 4,    /* wrong number of public input elements / inconsistent values */
+  ZKP_ERR_DEVICE = 5,        /* HIP failure or no device */
+  ZKP_ERR_NONCE = 6,         /* grinding nonce not found */
+  ZKP_ERR_OOM = 7,
+  ZKP_ERR_UNSUPPORTED_AIR = 8,
+  ZKP_ERR_ARGUMENT = 9
+} zkp_status;
+
+typedef struct zkp_ctx zkp_ctx;
+
+/* Per-proof transcript summary (debug / parity aid; optional out-param). */
+typedef struct zkp_transcript {
+  uint8_t trace_root[32];
+  uint8_t constraint_root[32];
+  uint8_t fri_roots[16][32];
+  uint8_t remainder_commitment[32];
+  uint32_t num_fri_layers;
+  uint32_t num_composition_columns;
+  uint64_t pow_nonce;
+  zkp_felt z;
+  uint32_t num_unique_queries;
+  uint64_t query_positions[255];
+} zkp_transcript;
+
+/* ---- context --------------------------------------------------------- */
+/* Bind to HIP device `device` (ordinal). One ctx per caller thread. */
+int zkp_ctx_create(int device, zkp_ctx** out);
+void zkp_ctx_destroy(zkp_ctx* ctx);
+/* Last error message for ctx (static storage owned by ctx). */
+const char* zkp_last_error(const zkp_ctx* ctx);
+void zkp_free(void* p);
+
+/* ---- whole-proof entry points (≙ Prover::prove) ------------------------ */
+/* Host trace (column-major, width*n felts) -> serialized proof
+ * (≙ winterfell `Proof::to_bytes()`, src/main.rs:229,425,469). */
+int zkp_prove(zkp_ctx* ctx, zkp_air_id air, const zkp_felt* trace_cols, uint32_t width,
+              uint64_t n, const zkp_felt* pub_elems, uint64_t n_pub,
+              const zkp_proof_options* opts, uint8_t** proof, uint64_t* proof_len,
+              zkp_transcript* transcript /* nullable */);
+
+/* Same, with the trace already resident in device memory (HBM). */
+int zkp_prove_device(zkp_ctx* ctx, zkp_air_id air, const void* d_trace_cols, uint32_t width,
+                     uint64_t n, const zkp_felt* pub_elems, uint64_t n_pub,
+                     const zkp_proof_options* opts, uint8_t** proof, uint64_t* proof_len,
+                     zkp_transcript* transcript /* nullable */);
+
+/* Device scratch helpers so callers (bench, tests) can keep traces in HBM. */
+int zkp_device_alloc(zkp_ctx* ctx, uint64_t bytes, void** d_ptr);
+int zkp_device_free(zkp_ctx* ctx, void* d_ptr);
+int zkp_copy_to_device(zkp_ctx* ctx, void* d_dst, const void* h_src, uint64_t bytes);
+int zkp_copy_to_host(zkp_ctx* ctx, void* h_dst, const void* d_src, uint64_t bytes);
+
+/* ---- stage entry points (for a winter-prover fork / stage parity) ------ */
+/* ≙ DefaultTraceLde::new (src/aggregation/prover.rs:216-224): interpolate each
+ * column over <w_n>, evaluate on 3*<w_{n*blowup}>, hash rows with BLAKE3 and
+ * build the Merkle tree. Outputs: LDE (column-major, natural domain order,
+ * width*n*blowup felts; nullable) and root. */
+int zkp_trace_lde_commit(zkp_ctx* ctx, const zkp_felt* trace_cols, uint32_t width, uint64_t n,
+                         uint32_t blowup, zkp_felt* lde_out /* nullable */, uint8_t root[32]);
+
+/* Batched BLAKE3 of rows of a column-major felt matrix (≙ RowMatrix::commit_to_rows
+ * leaf hashing) followed by MerkleTree::new; returns the root. */
+int zkp_merkle_commit_rows(zkp_ctx* ctx, const zkp_felt* cols, uint32_t width, uint64_t rows,
+                           uint8_t root[32]);
+
+/* Minimum-nonce grinding (sequential winterfell semantics):
+ * smallest nonce >= 1 with trailing_zeros(u64_le(BLAKE3(seed || nonce_le)[0..8])) >= bits. */
+int zkp_grind(zkp_ctx* ctx, const uint8_t seed[32], uint32_t bits, uint64_t* nonce);
+
+/* ---- profiling ------------------------------------------------------- */
+/* When enabled, every kernel launch is bracketed with HIP events on the
+ * stream it runs on; zkp_kernel_stats reports per-kernel launch count and
+ * total device milliseconds since the last reset. */
+int zkp_set_profiling(zkp_ctx* ctx, int enabled);
+int zkp_kernel_stats(zkp_ctx* ctx, const char* kernel_name, uint64_t* launches, double* total_ms);
+int zkp_reset_stats(zkp_ctx* ctx);
+/* Returns a newline-separated "name launches total_ms" table (free with zkp_free). */
+int zkp_kernel_stats_table(zkp_ctx* ctx, char** table);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ZKP_H */

@@ -1,0 +1,254 @@
+"""ctypes binding of libzkp.so (the HIP/gfx950 prover behind include/zkp.h).
+
+The library is built in-tree by __graft_entry__.build() / `make -C
+zk_stark_project_amd/csrc`. There is no CPU fallback: if the library or a
+gfx950 device is missing every compute call raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import numpy as np
+
+from .options import ProofOptions
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libzkp.so")
+
+ZKP_OK = 0
+STATUS = {
+    1: "invalid proof options", 2: "unsupported field extension", 3: "invalid trace shape",
+    4: "invalid public inputs", 5: "HIP device error", 6: "grinding nonce not found",
+    7: "out of device memory", 8: "unsupported AIR", 9: "invalid argument",
+}
+
+
+class ZkpError(RuntimeError):
+    def __init__(self, code, msg=""):
+        super().__init__(f"zkp error {code} ({STATUS.get(code, '?')}): {msg}")
+        self.code = code
+
+
+class Felt(ctypes.Structure):
+    _fields_ = [("lo", ctypes.c_uint64), ("hi", ctypes.c_uint64)]
+
+
+class Transcript(ctypes.Structure):
+    """`zkp_transcript` (include/zkp.h)."""
+    _fields_ = [
+        ("trace_root", ctypes.c_uint8 * 32),
+        ("constraint_root", ctypes.c_uint8 * 32),
+        ("fri_roots", (ctypes.c_uint8 * 32) * 16),
+        ("remainder_commitment", ctypes.c_uint8 * 32),
+        ("num_fri_layers", ctypes.c_uint32),
+        ("num_composition_columns", ctypes.c_uint32),
+        ("pow_nonce", ctypes.c_uint64),
+        ("z", Felt),
+        ("num_unique_queries", ctypes.c_uint32),
+        ("query_positions", ctypes.c_uint64 * 255),
+    ]
+
+    def summary(self) -> dict:
+        return {
+            "trace_root": bytes(self.trace_root).hex(),
+            "constraint_root": bytes(self.constraint_root).hex(),
+            "fri_roots": [bytes(self.fri_roots[i]).hex() for i in range(self.num_fri_layers)],
+            "remainder_commitment": bytes(self.remainder_commitment).hex(),
+            "pow_nonce": int(self.pow_nonce),
+            "z": int(self.z.lo) | (int(self.z.hi) << 64),
+            "num_composition_columns": int(self.num_composition_columns),
+            "query_positions": [int(self.query_positions[i]) for i in range(self.num_unique_queries)],
+        }
+
+
+# symbols declared in include/zkp.h (checked by tests/test_abi.py)
+EXPORTED = [
+    "zkp_ctx_create", "zkp_ctx_destroy", "zkp_last_error", "zkp_free", "zkp_prove",
+    "zkp_prove_device", "zkp_device_alloc", "zkp_device_free", "zkp_copy_to_device",
+    "zkp_copy_to_host", "zkp_trace_lde_commit", "zkp_merkle_commit_rows", "zkp_grind",
+    "zkp_set_profiling", "zkp_kernel_stats", "zkp_reset_stats", "zkp_kernel_stats_table",
+    "zkp_build_mimc_trace",
+]
+
+_lib = None
+_lock = threading.Lock()
+
+
+def load():
+    """Load libzkp.so, raising loudly if it was not built."""
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"{LIB_PATH} not built: run __graft_entry__.build() "
+                              "(make -C zk_stark_project_amd/csrc); there is no CPU fallback")
+        L = ctypes.CDLL(LIB_PATH)
+        vp, u32, u64, i32 = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int
+        pu8 = ctypes.POINTER(ctypes.c_uint8)
+        L.zkp_ctx_create.argtypes = [i32, ctypes.POINTER(vp)]
+        L.zkp_ctx_destroy.argtypes = [vp]
+        L.zkp_ctx_destroy.restype = None
+        L.zkp_last_error.argtypes = [vp]
+        L.zkp_last_error.restype = ctypes.c_char_p
+        L.zkp_free.argtypes = [vp]
+        L.zkp_free.restype = None
+        from .options import ProofOptionsC
+        popt = ctypes.POINTER(ProofOptionsC)
+        for name, trace_t in (("zkp_prove", vp), ("zkp_prove_device", vp)):
+            f = getattr(L, name)
+            f.argtypes = [vp, i32, trace_t, u32, u64, vp, u64, popt, ctypes.POINTER(pu8),
+                          ctypes.POINTER(u64), ctypes.POINTER(Transcript)]
+        L.zkp_device_alloc.argtypes = [vp, u64, ctypes.POINTER(vp)]
+        L.zkp_device_free.argtypes = [vp, vp]
+        L.zkp_copy_to_device.argtypes = [vp, vp, vp, u64]
+        L.zkp_copy_to_host.argtypes = [vp, vp, vp, u64]
+        L.zkp_trace_lde_commit.argtypes = [vp, vp, u32, u64, u32, vp, ctypes.c_char_p]
+        L.zkp_merkle_commit_rows.argtypes = [vp, vp, u32, u64, ctypes.c_char_p]
+        L.zkp_grind.argtypes = [vp, ctypes.c_char_p, u32, ctypes.POINTER(u64)]
+        L.zkp_set_profiling.argtypes = [vp, i32]
+        L.zkp_kernel_stats.argtypes = [vp, ctypes.c_char_p, ctypes.POINTER(u64), ctypes.POINTER(ctypes.c_double)]
+        L.zkp_reset_stats.argtypes = [vp]
+        L.zkp_kernel_stats_table.argtypes = [vp, ctypes.POINTER(ctypes.c_char_p)]
+        L.zkp_build_mimc_trace.argtypes = [ctypes.c_char_p, u64, vp]
+        L.zkp_build_mimc_trace.restype = i32
+        _lib = L
+        return L
+
+
+def mimc_trace(seed: int, n: int) -> np.ndarray:
+    """Host MiMC trace builder (serial chain) -> (n, 2) uint64."""
+    L = load()
+    out = np.empty((n, 2), dtype=np.uint64)
+    rc = L.zkp_build_mimc_trace(int(seed).to_bytes(16, "little"), n, out.ctypes.data)
+    if rc:
+        raise ZkpError(rc, "zkp_build_mimc_trace")
+    return out
+
+
+class Context:
+    """Owns one `zkp_ctx` (one HIP device, its streams and HBM buffers)."""
+
+    _default = None
+
+    def __init__(self, device: int = 0):
+        self.lib = load()
+        self.ptr = ctypes.c_void_p()
+        rc = self.lib.zkp_ctx_create(device, ctypes.byref(self.ptr))
+        if rc:
+            raise ZkpError(rc, "zkp_ctx_create")
+
+    @classmethod
+    def default(cls) -> "Context":
+        if cls._default is None:
+            cls._default = cls(0)
+        return cls._default
+
+    def close(self):
+        if self.ptr:
+            self.lib.zkp_ctx_destroy(self.ptr)
+            self.ptr = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc, what):
+        if rc:
+            msg = self.lib.zkp_last_error(self.ptr) or b""
+            raise ZkpError(rc, f"{what}: {msg.decode(errors='replace')}")
+
+    def prove(self, air_id: int, trace: np.ndarray, pub, options: ProofOptions, device_ptr=None):
+        """trace: (width, n, 2) uint64 host array (ignored when device_ptr is given)."""
+        w, n = int(trace.shape[0]), int(trace.shape[1])
+        pubb = b"".join(int(v).to_bytes(16, "little") for v in pub)
+        out = ctypes.POINTER(ctypes.c_uint8)()
+        olen = ctypes.c_uint64()
+        tr = Transcript()
+        oc = options.to_c()
+        if device_ptr is None:
+            trace = np.ascontiguousarray(trace, dtype=np.uint64)
+            rc = self.lib.zkp_prove(self.ptr, air_id, trace.ctypes.data, w, n, pubb, len(pub),
+                                    ctypes.byref(oc), ctypes.byref(out), ctypes.byref(olen), ctypes.byref(tr))
+        else:
+            rc = self.lib.zkp_prove_device(self.ptr, air_id, device_ptr, w, n, pubb, len(pub),
+                                           ctypes.byref(oc), ctypes.byref(out), ctypes.byref(olen),
+                                           ctypes.byref(tr))
+        self._check(rc, "zkp_prove")
+        data = ctypes.string_at(out, olen.value)
+        self.lib.zkp_free(out)
+        return data, tr
+
+    def prove_device(self, air_id, d_trace, width, n, pub, options):
+        shape = np.empty((width, n, 0))
+        return self.prove(air_id, shape, pub, options, device_ptr=d_trace)
+
+    # -- device memory ------------------------------------------------------
+    def alloc(self, nbytes: int) -> int:
+        p = ctypes.c_void_p()
+        self._check(self.lib.zkp_device_alloc(self.ptr, nbytes, ctypes.byref(p)), "zkp_device_alloc")
+        return p.value
+
+    def free(self, d_ptr: int):
+        self._check(self.lib.zkp_device_free(self.ptr, d_ptr), "zkp_device_free")
+
+    def to_device(self, d_ptr: int, host: np.ndarray):
+        host = np.ascontiguousarray(host)
+        self._check(self.lib.zkp_copy_to_device(self.ptr, d_ptr, host.ctypes.data, host.nbytes),
+                    "zkp_copy_to_device")
+
+    def to_host(self, host: np.ndarray, d_ptr: int):
+        self._check(self.lib.zkp_copy_to_host(self.ptr, host.ctypes.data, d_ptr, host.nbytes),
+                    "zkp_copy_to_host")
+
+    # -- stage entry points -------------------------------------------------
+    def trace_lde_commit(self, trace: np.ndarray, blowup: int, want_lde: bool = True):
+        trace = np.ascontiguousarray(trace, dtype=np.uint64)
+        w, n = trace.shape[0], trace.shape[1]
+        lde = np.empty((w, n * blowup, 2), dtype=np.uint64) if want_lde else None
+        root = ctypes.create_string_buffer(32)
+        self._check(self.lib.zkp_trace_lde_commit(self.ptr, trace.ctypes.data, w, n, blowup,
+                                                  lde.ctypes.data if want_lde else None, root),
+                    "zkp_trace_lde_commit")
+        return lde, root.raw
+
+    def merkle_commit_rows(self, cols: np.ndarray) -> bytes:
+        cols = np.ascontiguousarray(cols, dtype=np.uint64)
+        root = ctypes.create_string_buffer(32)
+        self._check(self.lib.zkp_merkle_commit_rows(self.ptr, cols.ctypes.data, cols.shape[0],
+                                                    cols.shape[1], root), "zkp_merkle_commit_rows")
+        return root.raw
+
+    def grind(self, seed: bytes, bits: int) -> int:
+        nonce = ctypes.c_uint64()
+        self._check(self.lib.zkp_grind(self.ptr, seed, bits, ctypes.byref(nonce)), "zkp_grind")
+        return nonce.value
+
+    # -- profiling ----------------------------------------------------------
+    def set_profiling(self, on: bool):
+        self._check(self.lib.zkp_set_profiling(self.ptr, 1 if on else 0), "zkp_set_profiling")
+
+    def reset_stats(self):
+        self._check(self.lib.zkp_reset_stats(self.ptr), "zkp_reset_stats")
+
+    def kernel_stats(self, name: str):
+        n = ctypes.c_uint64()
+        ms = ctypes.c_double()
+        self._check(self.lib.zkp_kernel_stats(self.ptr, name.encode(), ctypes.byref(n), ctypes.byref(ms)),
+                    "zkp_kernel_stats")
+        return n.value, ms.value
+
+    def stats_table(self) -> dict:
+        p = ctypes.c_char_p()
+        self._check(self.lib.zkp_kernel_stats_table(self.ptr, ctypes.byref(p)), "zkp_kernel_stats_table")
+        txt = p.value.decode()
+        self.lib.zkp_free(ctypes.cast(p, ctypes.c_void_p))
+        out = {}
+        for line in txt.splitlines():
+            name, cnt, ms = line.split()
+            out[name] = (int(cnt), float(ms))
+        return out
