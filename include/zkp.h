@@ -149,6 +149,13 @@ int zkp_merkle_commit_rows(zkp_ctx* ctx, const zkp_felt* cols, uint32_t width, u
  * smallest nonce >= 1 with trailing_zeros(u64_le(BLAKE3(seed || nonce_le)[0..8])) >= bits. */
 int zkp_grind(zkp_ctx* ctx, const uint8_t seed[32], uint32_t bits, uint64_t* nonce);
 
+/* ---- trace construction helper ---------------------------------------- */
+/* Host-side MiMC AIR trace: out[0] = seed mod p,
+ * out[i+1] = (out[i] + K[i % 64])^7 with K[j] = (j+1)*10^6
+ * (get_round_constants, src/helper.rs:404-406). Trace building, like
+ * `TraceTable` construction in the reference — not part of the proving path. */
+int zkp_build_mimc_trace(const uint8_t seed[16], uint64_t n, zkp_felt* out);
+
 /* ---- profiling ------------------------------------------------------- */
 /* When enabled, every kernel launch is bracketed with HIP events on the
  * stream it runs on; zkp_kernel_stats reports per-kernel launch count and

@@ -1,0 +1,91 @@
+"""GPU parity: libzkp.so (HIP, gfx950) vs the CPU oracle (oracle/liboracle.so)
+on the same seeded inputs — bit-exact (integer field arithmetic)."""
+import random
+
+import numpy as np
+import pytest
+
+import oracle_ref as O
+from zk_stark_project_amd import (AIR_GLOBAL_UPDATE, AIR_MIMC, GlobalUpdateProver, MimcProver,
+                                  ProofOptions, TraceTable)
+from zk_stark_project_amd.field import P, to_bytes
+from zk_stark_project_amd.helper import f64_to_felt
+
+pytestmark = pytest.mark.gpu
+
+
+def rand_trace(w, n, seed):
+    rng = np.random.default_rng(seed)
+    a = rng.integers(0, 2**64, size=(w, n, 2), dtype=np.uint64)
+    a[..., 1] &= np.uint64(0x7FFFFFFFFFFFFFFF)  # < p
+    return a
+
+
+@pytest.mark.parametrize("w,n,blowup", [(1, 8, 2), (1, 64, 8), (3, 256, 4), (120, 16, 16), (2, 1024, 8)])
+def test_trace_lde_commit_matches_oracle(ctx, w, n, blowup):
+    tr = rand_trace(w, n, seed=w * 1000 + n)
+    lde, root = ctx.trace_lde_commit(tr, blowup)
+    olde, oroot = O.trace_lde(tr.tobytes(), w, n, blowup)
+    assert lde.tobytes() == olde
+    assert root == oroot
+
+
+@pytest.mark.parametrize("w,rows", [(1, 2), (1, 1024), (7, 64), (64, 32), (65, 16), (120, 64), (255, 8)])
+def test_merkle_rows_matches_oracle(ctx, w, rows):
+    m = rand_trace(w, rows, seed=rows + w)
+    assert ctx.merkle_commit_rows(m) == O.merkle_rows(m.tobytes(), w, rows)
+
+
+@pytest.mark.parametrize("bits", [0, 1, 8, 16])
+def test_grind_min_nonce(ctx, bits):
+    seed = bytes(range(32))
+    g = ctx.grind(seed, bits)
+    assert g == O.grind(seed, bits)
+    assert g >= 1
+
+
+def mimc_case(n, opts):
+    p = MimcProver(opts)
+    trace = p.build_trace(42 * 10**6, n)
+    return p, trace
+
+
+@pytest.mark.parametrize("n,blowup,q,grind", [(64, 8, 40, 8), (128, 8, 40, 0), (256, 16, 24, 4),
+                                              (1024, 8, 40, 16), (4096, 8, 40, 12)])
+def test_mimc_proof_bit_exact(ctx, n, blowup, q, grind):
+    opts = ProofOptions(q, blowup, grind)
+    p, trace = mimc_case(n, opts)
+    pub = to_bytes(p.get_pub_inputs(trace).to_elements())
+    gpu, gtr = ctx.prove(AIR_MIMC, trace.data, p.get_pub_inputs(trace).to_elements(), opts)
+    ref, otr = O.prove(AIR_MIMC, trace.to_bytes(), 1, n, pub, opts)
+    assert bytes(gtr.trace_root) == bytes(otr.trace_root)
+    assert bytes(gtr.constraint_root) == bytes(otr.constraint_root)
+    assert gtr.pow_nonce == otr.pow_nonce
+    assert gpu == ref
+    assert O.verify(AIR_MIMC, gpu, pub, opts) == 0
+
+
+def gu_prover(ndev, n, opts, seed):
+    rnd = random.Random(seed)
+    r = lambda: rnd.randrange(2**64)
+    gw = [[r() for _ in range(9)] for _ in range(6)]
+    gb = [r() for _ in range(6)]
+    lw = [[[r() for _ in range(9)] for _ in range(6)] for _ in range(ndev)]
+    lb = [[r() for _ in range(6)] for _ in range(ndev)]
+    return GlobalUpdateProver(opts, gw, gb, lw, lb, f64_to_felt(ndev), trace_length=n,
+                              blinding=[r() for _ in range(60)])
+
+
+@pytest.mark.parametrize("ndev,n", [(2, 8), (6, 64), (30, 256)])
+def test_global_update_proof_bit_exact(ctx, ndev, n):
+    opts = ProofOptions(40, 16, 8)
+    p = gu_prover(ndev, n, opts, seed=ndev)
+    trace = p.build_trace()
+    pub_el = p.get_pub_inputs(trace).to_elements()
+    pub = to_bytes(pub_el)
+    gpu, gtr = ctx.prove(AIR_GLOBAL_UPDATE, trace.data, pub_el, opts)
+    ref, otr = O.prove(AIR_GLOBAL_UPDATE, trace.to_bytes(), 120, n, pub, opts)
+    assert bytes(gtr.trace_root) == bytes(otr.trace_root)
+    assert bytes(gtr.constraint_root) == bytes(otr.constraint_root)
+    assert gpu == ref
+    assert O.verify(AIR_GLOBAL_UPDATE, gpu, pub, opts) == 0

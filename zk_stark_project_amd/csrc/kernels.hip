@@ -1,0 +1,644 @@
+// kernels.hip — CDNA4 (gfx950) kernels of the STARK prover hot path.
+//
+// All arithmetic is exact f128 integer arithmetic, so results are
+// order-independent and bit-identical to the CPU restatement in oracle/.
+// Layouts (see DESIGN.md "Data layout in HBM"):
+//  * coefficient arrays: bit-reversed order, scaled by n (output of the
+//    Gentleman-Sande inverse NTT, never permuted);
+//  * LDE matrices: coset-major, column c, coset j, row t at (c*B + j)*n + t,
+//    holding P_c(g * w_N^j * w_n^t) = LDE index i = j + B*t;
+//  * Merkle trees: nodes[1..2L) of 8-word digests, leaves at nodes[L..2L).
+#include "zkp_internal.hpp"
+#include "blake3.hpp"
+
+using namespace fp;
+
+#define TPB 256
+
+namespace {
+
+__device__ __forceinline__ uint32_t rev_bits(uint32_t x, uint32_t bits) {
+  return bits == 0 ? 0u : (__brev(x) >> (32 - bits));
+}
+
+// w_N^e for e < N (table holds e < N/2; w_N^(N/2) = -1)
+__device__ __forceinline__ felt tw_full(const felt* tw, uint64_t e, uint32_t logN) {
+  uint64_t half = 1ull << (logN - 1);
+  return e < half ? tw[e] : neg(tw[e - half]);
+}
+
+__device__ __forceinline__ void store_digest(uint32_t* dst, const uint32_t d[8]) {
+  uint4* p = reinterpret_cast<uint4*>(dst);
+  p[0] = make_uint4(d[0], d[1], d[2], d[3]);
+  p[1] = make_uint4(d[4], d[5], d[6], d[7]);
+}
+__device__ __forceinline__ void load_digest(const uint32_t* src, uint32_t d[8]) {
+  const uint4* p = reinterpret_cast<const uint4*>(src);
+  uint4 a = p[0], b = p[1];
+  d[0] = a.x; d[1] = a.y; d[2] = a.z; d[3] = a.w;
+  d[4] = b.x; d[5] = b.y; d[6] = b.z; d[7] = b.w;
+}
+
+// --------------------------------------------------------------------- NTT
+struct NttKArgs {
+  const felt* src;
+  felt* dst;
+  const felt* scale;
+  const felt* tw;
+  uint64_t src_stride, dst_stride;
+  uint32_t src_div, scale_mod;
+  uint32_t logn, s0, K, lo, T, Tl, logT, logTl, tw_shift, dit;
+};
+
+// One LDS pass of K radix-2 stages over T interleaved groups of 2^K elements.
+// Group g = (hi, l): elements hi*2^(lo+K) + q*2^lo + l, q < 2^K. Loads are
+// ordered so each wave reads runs of Tl (>= 8 when lo allows) contiguous felts.
+__global__ __launch_bounds__(TPB) void k_ntt_pass(NttKArgs a) {
+  extern __shared__ felt lds[];
+  const uint32_t bidx = blockIdx.y;
+  const felt* src = a.src + (uint64_t)(bidx / a.src_div) * a.src_stride;
+  felt* dst = a.dst + (uint64_t)bidx * a.dst_stride;
+  const felt* scale = a.scale ? a.scale + ((uint64_t)(bidx % a.scale_mod) << a.logn) : nullptr;
+  const uint32_t K = a.K, T = a.T, Tl = a.Tl, lo = a.lo;
+  const uint32_t E = T << K;
+  const uint64_t g0 = (uint64_t)blockIdx.x * T;
+  const uint64_t hi0 = g0 >> lo;
+  const uint64_t l0 = (Tl == T) ? (g0 & ((1ull << lo) - 1)) : 0;
+  const uint32_t qmask = (1u << K) - 1;
+
+  for (uint32_t e = threadIdx.x; e < E; e += TPB) {
+    uint32_t ll = e & (Tl - 1);
+    uint32_t rest = e >> a.logTl;
+    uint32_t q = rest & qmask;
+    uint32_t hl = rest >> K;
+    uint64_t addr = ((hi0 + hl) << (lo + K)) + ((uint64_t)q << lo) + l0 + ll;
+    felt v = src[addr];
+    if (scale) v = mul(v, scale[addr]);
+    lds[(q << a.logT) + (hl * Tl) + ll] = v;
+  }
+  __syncthreads();
+  for (uint32_t ls = 0; ls < K; ls++) {
+    const uint32_t s = a.s0 + ls;
+    const uint32_t pbit = a.dit ? ls : (K - 1 - ls);
+    const uint32_t twsh = a.dit ? (a.logn - 1 - s + a.tw_shift) : (s + a.tw_shift);
+    const uint32_t pmask = (1u << pbit) - 1;
+    for (uint32_t bf = threadIdx.x; bf < (E >> 1); bf += TPB) {
+      uint32_t gg = bf & (T - 1);
+      uint32_t qq = bf >> a.logT;
+      uint32_t q = ((qq >> pbit) << (pbit + 1)) | (qq & pmask);
+      uint32_t q2 = q | (1u << pbit);
+      uint64_t l = l0 + (gg & (Tl - 1));
+      uint64_t j = ((uint64_t)(q & pmask) << lo) | l;
+      felt w = a.tw[j << twsh];
+      uint32_t i0 = (q << a.logT) + gg, i1 = (q2 << a.logT) + gg;
+      felt x = lds[i0], y = lds[i1];
+      if (a.dit) {
+        felt t = mul(y, w);
+        lds[i0] = add(x, t);
+        lds[i1] = sub(x, t);
+      } else {
+        lds[i0] = add(x, y);
+        lds[i1] = mul(sub(x, y), w);
+      }
+    }
+    __syncthreads();
+  }
+  for (uint32_t e = threadIdx.x; e < E; e += TPB) {
+    uint32_t ll = e & (Tl - 1);
+    uint32_t rest = e >> a.logTl;
+    uint32_t q = rest & qmask;
+    uint32_t hl = rest >> K;
+    uint64_t addr = ((hi0 + hl) << (lo + K)) + ((uint64_t)q << lo) + l0 + ll;
+    dst[addr] = lds[(q << a.logT) + (hl * Tl) + ll];
+  }
+}
+
+// ------------------------------------------------------------------ tables
+__global__ void k_expand_powers(felt* out, uint64_t count, const felt* lo_tab, const felt* hi_tab) {
+  for (uint64_t e = blockIdx.x * (uint64_t)TPB + threadIdx.x; e < count; e += (uint64_t)gridDim.x * TPB)
+    out[e] = mul(lo_tab[e & 2047], hi_tab[e >> 11]);
+}
+
+__global__ void k_build_coset_scale(felt* S, uint32_t logn, uint32_t B, const felt* tw, uint32_t logN,
+                                    const felt* glo, const felt* ghi, felt ninv) {
+  uint64_t total = (uint64_t)B << logn;
+  for (uint64_t idx = blockIdx.x * (uint64_t)TPB + threadIdx.x; idx < total; idx += (uint64_t)gridDim.x * TPB) {
+    uint64_t j = idx >> logn;
+    uint32_t p = (uint32_t)(idx & ((1ull << logn) - 1));
+    uint32_t k = rev_bits(p, logn);
+    felt gk = mul(glo[k & 2047], ghi[k >> 11]);
+    S[idx] = mul(ninv, mul(gk, tw_full(tw, j * k, logN)));
+  }
+}
+
+__global__ void k_build_ginv(felt* Gi, uint32_t logn, const felt* gilo, const felt* gihi) {
+  uint64_t n = 1ull << logn;
+  for (uint64_t p = blockIdx.x * (uint64_t)TPB + threadIdx.x; p < n; p += (uint64_t)gridDim.x * TPB) {
+    uint32_t k = rev_bits((uint32_t)p, logn);
+    Gi[p] = mul(gilo[k & 2047], gihi[k >> 11]);
+  }
+}
+
+// ------------------------------------------------------------------ hashing
+__global__ __launch_bounds__(TPB) void k_leaf_hash_lde(const felt* __restrict__ lde, uint32_t cols, uint32_t logB,
+                                                       uint64_t n, uint32_t* __restrict__ nodes, uint64_t L) {
+  uint64_t i = blockIdx.x * (uint64_t)TPB + threadIdx.x;
+  if (i >= L) return;
+  uint64_t j = i & ((1ull << logB) - 1), t = i >> logB;
+  const felt* base = lde + j * n + t;
+  const uint64_t cstride = n << logB;
+  uint32_t d[8];
+  b3::hash_felts([&](uint32_t c) { return base[c * cstride]; }, cols, d);
+  store_digest(nodes + (L + i) * 8, d);
+}
+
+__global__ __launch_bounds__(TPB) void k_leaf_hash_fri(const felt* __restrict__ E, uint64_t R, uint32_t F,
+                                                       uint32_t* __restrict__ nodes) {
+  uint64_t r = blockIdx.x * (uint64_t)TPB + threadIdx.x;
+  if (r >= R) return;
+  uint32_t d[8];
+  b3::hash_felts([&](uint32_t k) { return E[r + k * R]; }, F, d);
+  store_digest(nodes + (R + r) * 8, d);
+}
+
+// nodes[s + i] = merge(nodes[2(s+i)], nodes[2(s+i)+1]) for i < s
+__global__ __launch_bounds__(TPB) void k_merkle_level(uint32_t* nodes, uint64_t s) {
+  uint64_t i = blockIdx.x * (uint64_t)TPB + threadIdx.x;
+  if (i >= s) return;
+  uint64_t node = s + i;
+  uint32_t m[16];
+  load_digest(nodes + 2 * node * 8, m);
+  load_digest(nodes + (2 * node + 1) * 8, m + 8);
+  uint32_t out[8];
+  b3::set_iv(out);
+  b3::compress(out, m, 0, 64, b3::CHUNK_START | b3::CHUNK_END | b3::ROOT);
+  store_digest(nodes + node * 8, out);
+}
+
+// remaining top levels (s_start .. 1) inside one workgroup
+__global__ __launch_bounds__(1024) void k_merkle_top(uint32_t* nodes, uint64_t s_start) {
+  for (uint64_t s = s_start; s >= 1; s >>= 1) {
+    for (uint64_t i = threadIdx.x; i < s; i += blockDim.x) {
+      uint64_t node = s + i;
+      uint32_t m[16];
+      load_digest(nodes + 2 * node * 8, m);
+      load_digest(nodes + (2 * node + 1) * 8, m + 8);
+      uint32_t out[8];
+      b3::set_iv(out);
+      b3::compress(out, m, 0, 64, b3::CHUNK_START | b3::CHUNK_END | b3::ROOT);
+      store_digest(nodes + node * 8, out);
+    }
+    __threadfence_block();
+    __syncthreads();
+  }
+}
+
+struct SeedArg {
+  uint32_t w[8];
+};
+
+__global__ __launch_bounds__(TPB) void k_grind(SeedArg seed, uint64_t base, uint64_t count, uint32_t bits,
+                                               unsigned long long* result) {
+  uint64_t i = blockIdx.x * (uint64_t)TPB + threadIdx.x;
+  if (i >= count) return;
+  uint64_t nonce = base + i;
+  uint32_t m[16];
+#pragma unroll
+  for (int k = 0; k < 8; k++) m[k] = seed.w[k];
+  m[8] = (uint32_t)nonce;
+  m[9] = (uint32_t)(nonce >> 32);
+#pragma unroll
+  for (int k = 10; k < 16; k++) m[k] = 0;
+  uint32_t out[8];
+  b3::set_iv(out);
+  b3::compress(out, m, 0, 40, b3::CHUNK_START | b3::CHUNK_END | b3::ROOT);
+  uint64_t h = (uint64_t)out[0] | ((uint64_t)out[1] << 32);
+  uint32_t tz = h == 0 ? 64u : (uint32_t)__builtin_ctzll(h);
+  if (tz >= bits) atomicMin(result, (unsigned long long)nonce);
+}
+
+// -------------------------------------------------------------- constraints
+constexpr int EVAL_CH = 8;  // points per thread (batch-inversion chunk)
+
+__device__ __forceinline__ void batch_inverse(felt* v, int n) {
+  felt pre[EVAL_CH];
+  felt acc = one();
+#pragma unroll
+  for (int i = 0; i < EVAL_CH; i++) {
+    if (i < n) { pre[i] = acc; acc = mul(acc, v[i]); }
+  }
+  felt ia = inv(acc);
+#pragma unroll
+  for (int i = EVAL_CH - 1; i >= 0; i--) {
+    if (i < n) {
+      felt t = mul(ia, pre[i]);
+      ia = mul(ia, v[i]);
+      v[i] = t;
+    }
+  }
+}
+
+__global__ __launch_bounds__(TPB) void k_eval_mimc(EvalCommon c, MimcEvalArgs a, const felt* __restrict__ lde,
+                                                   felt* __restrict__ comp) {
+  const uint64_t M = 1ull << (c.logn + c.logce);
+  const uint64_t base = (blockIdx.x * (uint64_t)TPB + threadIdx.x) * EVAL_CH;
+  if (base >= M) return;
+  const int cnt = (int)((M - base) < EVAL_CH ? (M - base) : EVAL_CH);
+  const uint64_t n = 1ull << c.logn;
+  const uint32_t sh = c.logB - c.logce;
+  const uint32_t xsh = c.logN - c.logce - c.logn;
+  const uint64_t kmask = (64ull << c.logce) - 1;
+  felt tpart[EVAL_CH], bnum[EVAL_CH], den[EVAL_CH];
+#pragma unroll
+  for (int k = 0; k < EVAL_CH; k++) {
+    if (k >= cnt) { den[k] = one(); continue; }
+    uint64_t s = base + k;
+    uint64_t idx = s << sh;
+    uint64_t j = idx & ((1ull << c.logB) - 1), t = idx >> c.logB;
+    felt cur = lde[j * n + t];
+    felt nxt = lde[j * n + ((t + 1) & (n - 1))];
+    felt kv = a.kper[s & kmask];
+    felt x = mul(c.g, tw_full(c.tw, s << xsh, c.logN));
+    felt u = add(cur, kv);
+    felt u2 = sqr(u), u3 = mul(u2, u), u6 = sqr(u3), u7 = mul(u6, u);
+    felt tr = mul(a.coef_t, sub(nxt, u7));
+    felt e0 = sub(x, one()), e1 = sub(x, c.w_last);
+    tpart[k] = mul(mul(tr, e1), c.zinv[s & ((1ull << c.logce) - 1)]);
+    bnum[k] = add(mul(mul(a.b0, sub(cur, a.v0)), e1), mul(mul(a.b1, sub(cur, a.v1)), e0));
+    den[k] = mul(e0, e1);
+  }
+  batch_inverse(den, cnt);
+#pragma unroll
+  for (int k = 0; k < EVAL_CH; k++)
+    if (k < cnt) comp[base + k] = add(tpart[k], mul(bnum[k], den[k]));
+}
+
+__global__ __launch_bounds__(TPB) void k_eval_linear(EvalCommon c, LinearEvalArgs a, const felt* __restrict__ lde,
+                                                     felt* __restrict__ comp) {
+  const uint64_t M = 1ull << (c.logn + c.logce);
+  const uint64_t base = (blockIdx.x * (uint64_t)TPB + threadIdx.x) * EVAL_CH;
+  if (base >= M) return;
+  const int cnt = (int)((M - base) < EVAL_CH ? (M - base) : EVAL_CH);
+  const uint64_t n = 1ull << c.logn;
+  const uint32_t sh = c.logB - c.logce;
+  const uint32_t xsh = c.logN - c.logce - c.logn;
+  const uint64_t cstride = n << c.logB;
+  felt tpart[EVAL_CH], bnum[EVAL_CH], den[EVAL_CH];
+#pragma unroll
+  for (int k = 0; k < EVAL_CH; k++) {
+    if (k >= cnt) { den[k] = one(); continue; }
+    uint64_t s = base + k;
+    uint64_t idx = s << sh;
+    uint64_t j = idx & ((1ull << c.logB) - 1), t = idx >> c.logB;
+    const felt* pc = lde + j * n + t;
+    const felt* pn = lde + j * n + ((t + 1) & (n - 1));
+    felt tr = zero(), bs = zero();
+    for (uint32_t col = 0; col < a.width; col++) {
+      felt cur = pc[col * cstride], nxt = pn[col * cstride];
+      tr = add(tr, add(mul(a.coefs[col], nxt), mul(a.coefs[a.width + col], cur)));
+      bs = add(bs, mul(a.coefs[2 * a.width + col], cur));
+    }
+    felt x = mul(c.g, tw_full(c.tw, s << xsh, c.logN));
+    tpart[k] = mul(mul(tr, sub(x, c.w_last)), c.zinv[s & ((1ull << c.logce) - 1)]);
+    bnum[k] = sub(bs, a.bconst);
+    den[k] = sub(x, a.w_bstep);
+  }
+  batch_inverse(den, cnt);
+#pragma unroll
+  for (int k = 0; k < EVAL_CH; k++)
+    if (k < cnt) comp[base + k] = add(tpart[k], mul(bnum[k], den[k]));
+}
+
+__global__ void k_segment(const felt* __restrict__ difout, uint32_t logn, uint32_t logce, uint32_t C,
+                          const felt* __restrict__ Gi, const felt* __restrict__ scales, felt* __restrict__ out) {
+  uint64_t n = 1ull << logn, total = (uint64_t)C << logn;
+  for (uint64_t idx = blockIdx.x * (uint64_t)TPB + threadIdx.x; idx < total; idx += (uint64_t)gridDim.x * TPB) {
+    uint32_t h = (uint32_t)(idx >> logn);
+    uint64_t p = idx & (n - 1);
+    felt v = difout[(p << logce) + rev_bits(h, logce)];
+    out[idx] = mul(mul(v, Gi[p]), scales[h]);
+  }
+}
+
+// bit-reversed polynomial evaluation: tree with level multipliers x^(2^l)
+constexpr uint32_t OOD_LOGE = 11;
+__global__ __launch_bounds__(TPB) void k_eval_bitrev(const felt* __restrict__ arrays, uint32_t logn, uint32_t logE,
+                                                     const felt* __restrict__ pw0, const felt* __restrict__ pw1,
+                                                     felt* __restrict__ partial) {
+  __shared__ felt s0[1u << OOD_LOGE];
+  __shared__ felt s1[1u << OOD_LOGE];
+  const uint32_t E = 1u << logE;
+  const felt* src = arrays + ((uint64_t)blockIdx.y << logn) + ((uint64_t)blockIdx.x << logE);
+  for (uint32_t e = threadIdx.x; e < E; e += TPB) {
+    felt v = src[e];
+    s0[e] = v;
+    s1[e] = v;
+  }
+  __syncthreads();
+  for (uint32_t l = 0; l < logE; l++) {
+    const uint32_t d = 1u << l;
+    const felt m0 = pw0[logn - 1 - l], m1 = pw1[logn - 1 - l];
+    for (uint32_t i = threadIdx.x; i < (E >> (l + 1)); i += TPB) {
+      uint32_t p = i << (l + 1);
+      s0[p] = add(s0[p], mul(m0, s0[p + d]));
+      s1[p] = add(s1[p], mul(m1, s1[p + d]));
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    uint64_t o = ((uint64_t)blockIdx.y * gridDim.x + blockIdx.x) * 2;
+    partial[o] = s0[0];
+    partial[o + 1] = s1[0];
+  }
+}
+
+__global__ __launch_bounds__(TPB) void k_deep(DeepArgs a, felt* __restrict__ out) {
+  const uint64_t N = 1ull << a.logN;
+  const uint64_t base = (blockIdx.x * (uint64_t)TPB + threadIdx.x) * EVAL_CH;
+  if (base >= N) return;
+  const int cnt = (int)((N - base) < EVAL_CH ? (N - base) : EVAL_CH);
+  const uint64_t n = 1ull << a.logn;
+  const uint64_t cstride = n << a.logB;
+  felt num[EVAL_CH], den[EVAL_CH];
+#pragma unroll
+  for (int k = 0; k < EVAL_CH; k++) {
+    if (k >= cnt) { den[k] = one(); continue; }
+    uint64_t i = base + k;
+    uint64_t j = i & ((1ull << a.logB) - 1), t = i >> a.logB;
+    const uint64_t off = j * n + t;
+    felt A = zero(), Bh = zero();
+    for (uint32_t c = 0; c < a.w; c++) A = add(A, mul(a.gamma[c], a.tlde[c * cstride + off]));
+    for (uint32_t h = 0; h < a.C; h++) Bh = add(Bh, mul(a.gamma[a.w + h], a.clde[h * cstride + off]));
+    felt x = mul(a.g, tw_full(a.tw, i, a.logN));
+    felt e1 = sub(x, a.z), e2 = sub(x, a.zg);
+    num[k] = add(mul(sub(add(A, Bh), a.kz), e2), mul(sub(A, a.kzg), e1));
+    den[k] = mul(e1, e2);
+  }
+  batch_inverse(den, cnt);
+#pragma unroll
+  for (int k = 0; k < EVAL_CH; k++)
+    if (k < cnt) out[base + k] = mul(num[k], den[k]);
+}
+
+// fold-by-16: u = iDFT16(row) (unscaled), result = (1/16) sum_k u_k beta^k,
+// beta = alpha / x_r; eps_inv[m] = w_16^-m for m < 8, eps_inv[8] = 1/16
+__global__ __launch_bounds__(TPB) void k_fri_fold16(const felt* __restrict__ E, uint64_t R, felt alpha,
+                                                    felt off_inv, const felt* __restrict__ itw, uint32_t xsh,
+                                                    const felt* __restrict__ eps_inv, felt* __restrict__ out) {
+  uint64_t r = blockIdx.x * (uint64_t)TPB + threadIdx.x;
+  if (r >= R) return;
+  felt v[16];
+#pragma unroll
+  for (int k = 0; k < 16; k++) v[k] = E[r + k * R];
+  // Gentleman-Sande, natural in -> bit-reversed out
+#pragma unroll
+  for (int half = 8; half >= 1; half >>= 1) {
+#pragma unroll
+    for (int blk = 0; blk < 16; blk += 2 * half) {
+#pragma unroll
+      for (int i = 0; i < half; i++) {
+        felt x = v[blk + i], y = v[blk + i + half];
+        v[blk + i] = add(x, y);
+        felt d = sub(x, y);
+        const int m = i * (8 / half);
+        v[blk + i + half] = m == 0 ? d : mul(d, eps_inv[m]);
+      }
+    }
+  }
+  felt beta = mul(alpha, mul(off_inv, itw[r << xsh]));
+  // Horner over k = 15..0 with u_k = v[rev4(k)]
+  const int rev4[16] = {0, 8, 4, 12, 2, 10, 6, 14, 1, 9, 5, 13, 3, 11, 7, 15};
+  felt acc = v[rev4[15]];
+#pragma unroll
+  for (int k = 14; k >= 0; k--) acc = add(mul(acc, beta), v[rev4[k]]);
+  out[r] = mul(acc, eps_inv[8]);
+}
+
+__global__ void k_gather_felts(const felt* __restrict__ src, const uint64_t* __restrict__ idx, felt* __restrict__ out,
+                               uint64_t count) {
+  uint64_t i = blockIdx.x * (uint64_t)TPB + threadIdx.x;
+  if (i < count) out[i] = src[idx[i]];
+}
+
+__global__ void k_gather_digests(const uint32_t* __restrict__ nodes, const uint64_t* __restrict__ idx,
+                                 uint32_t* __restrict__ out, uint64_t count) {
+  uint64_t i = blockIdx.x * (uint64_t)TPB + threadIdx.x;
+  if (i < count) {
+    uint32_t d[8];
+    load_digest(nodes + idx[i] * 8, d);
+    store_digest(out + i * 8, d);
+  }
+}
+
+inline uint32_t blocks_for(uint64_t n, uint32_t per_block = TPB) {
+  uint64_t b = (n + per_block - 1) / per_block;
+  return (uint32_t)(b == 0 ? 1 : b);
+}
+inline uint32_t grid_stride_blocks(uint64_t n) {
+  uint64_t b = (n + TPB - 1) / TPB;
+  if (b > 8192) b = 8192;
+  return (uint32_t)(b == 0 ? 1 : b);
+}
+inline uint32_t ilog2_u64(uint64_t v) {
+  uint32_t l = 0;
+  while ((1ull << l) < v) l++;
+  return l;
+}
+
+}  // namespace
+
+// ======================================================================= host
+hipEvent_t Prof::get_event() {
+  if (!pool.empty()) {
+    hipEvent_t e = pool.back();
+    pool.pop_back();
+    return e;
+  }
+  hipEvent_t e;
+  (void)hipEventCreate(&e);
+  return e;
+}
+void Prof::begin(const char* name, hipStream_t s) {
+  if (!enabled) return;
+  ProfRec r;
+  r.name = name;
+  r.start = get_event();
+  r.stop = get_event();
+  (void)hipEventRecord(r.start, s);
+  pending.push_back(r);
+}
+void Prof::end(hipStream_t s) {
+  if (!enabled) return;
+  (void)hipEventRecord(pending.back().stop, s);
+}
+
+#define LAUNCH(prof, name, stream, ...)                        \
+  do {                                                          \
+    (prof).begin(name, stream);                                 \
+    __VA_ARGS__;                                                \
+    (prof).end(stream);                                         \
+  } while (0)
+
+std::vector<NttPass> ntt_plan(uint32_t logn, bool dit) {
+  const uint32_t KMAX = 8, LOGE = 12;
+  std::vector<NttPass> out;
+  if (logn == 0) return out;
+  uint32_t npass = (logn + KMAX - 1) / KMAX;
+  uint32_t s0 = 0;
+  for (uint32_t p = 0; p < npass; p++) {
+    uint32_t K = logn / npass + (p < logn % npass ? 1 : 0);
+    NttPass ps;
+    ps.logn = logn;
+    ps.s0 = s0;
+    ps.K = K;
+    ps.lo = dit ? s0 : logn - s0 - K;
+    uint32_t logG = logn - K;
+    uint32_t logT = LOGE - K < logG ? LOGE - K : logG;
+    uint32_t logTl = logT < ps.lo ? logT : ps.lo;
+    ps.T = 1u << logT;
+    ps.Tl = 1u << logTl;
+    out.push_back(ps);
+    s0 += K;
+  }
+  return out;
+}
+
+void launch_ntt(Prof& prof, hipStream_t s, const NttBatch& b, uint32_t logn, bool dit, const felt* tw,
+                uint32_t logN) {
+  auto plan = ntt_plan(logn, dit);
+  bool first = true;
+  for (const auto& ps : plan) {
+    NttKArgs a;
+    a.src = first ? b.src : b.dst;
+    a.dst = b.dst;
+    a.scale = first ? b.scale : nullptr;
+    a.tw = tw;
+    a.src_stride = first ? b.src_stride : b.dst_stride;
+    a.dst_stride = b.dst_stride;
+    a.src_div = first ? b.src_div : 1;
+    a.scale_mod = b.scale_mod ? b.scale_mod : 1;
+    a.logn = logn;
+    a.s0 = ps.s0;
+    a.K = ps.K;
+    a.lo = ps.lo;
+    a.T = ps.T;
+    a.Tl = ps.Tl;
+    a.logT = ilog2_u64(ps.T);
+    a.logTl = ilog2_u64(ps.Tl);
+    a.tw_shift = logN - logn;
+    a.dit = dit ? 1 : 0;
+    uint64_t groups = 1ull << (logn - ps.K);
+    dim3 grid((uint32_t)(groups / ps.T), b.batches);
+    size_t shmem = (size_t)(ps.T << ps.K) * sizeof(felt);
+    LAUNCH(prof, dit ? "ntt_dit_pass" : "ntt_dif_pass", s,
+           hipLaunchKernelGGL(k_ntt_pass, grid, dim3(TPB), shmem, s, a));
+    first = false;
+  }
+}
+
+void launch_expand_powers(Prof& prof, hipStream_t s, felt* out, uint64_t count, const felt* lo_tab,
+                          const felt* hi_tab) {
+  LAUNCH(prof, "expand_powers", s,
+         hipLaunchKernelGGL(k_expand_powers, dim3(grid_stride_blocks(count)), dim3(TPB), 0, s, out, count, lo_tab,
+                            hi_tab));
+}
+
+void launch_build_coset_scale(Prof& prof, hipStream_t s, felt* S, uint32_t logn, uint32_t B, const felt* tw,
+                              uint32_t logN, const felt* glo, const felt* ghi, felt ninv) {
+  LAUNCH(prof, "build_coset_scale", s,
+         hipLaunchKernelGGL(k_build_coset_scale, dim3(grid_stride_blocks((uint64_t)B << logn)), dim3(TPB), 0, s, S,
+                            logn, B, tw, logN, glo, ghi, ninv));
+}
+
+void launch_build_ginv(Prof& prof, hipStream_t s, felt* Gi, uint32_t logn, const felt* gilo, const felt* gihi) {
+  LAUNCH(prof, "build_ginv", s,
+         hipLaunchKernelGGL(k_build_ginv, dim3(grid_stride_blocks(1ull << logn)), dim3(TPB), 0, s, Gi, logn, gilo,
+                            gihi));
+}
+
+void launch_leaf_hash_lde(Prof& prof, hipStream_t s, const felt* lde, uint32_t cols, uint32_t logB, uint64_t n,
+                          uint32_t* nodes, uint64_t L) {
+  LAUNCH(prof, "leaf_hash_lde", s,
+         hipLaunchKernelGGL(k_leaf_hash_lde, dim3(blocks_for(L)), dim3(TPB), 0, s, lde, cols, logB, n, nodes, L));
+}
+
+void launch_leaf_hash_fri(Prof& prof, hipStream_t s, const felt* E, uint64_t R, uint32_t F, uint32_t* nodes) {
+  LAUNCH(prof, "leaf_hash_fri", s,
+         hipLaunchKernelGGL(k_leaf_hash_fri, dim3(blocks_for(R)), dim3(TPB), 0, s, E, R, F, nodes));
+}
+
+void launch_merkle_tree(Prof& prof, hipStream_t s, uint32_t* nodes, uint64_t L) {
+  uint64_t lvl = L / 2;
+  for (; lvl >= 2048; lvl >>= 1)
+    LAUNCH(prof, "merkle_level", s,
+           hipLaunchKernelGGL(k_merkle_level, dim3(blocks_for(lvl)), dim3(TPB), 0, s, nodes, lvl));
+  if (lvl >= 1)
+    LAUNCH(prof, "merkle_top", s, hipLaunchKernelGGL(k_merkle_top, dim3(1), dim3(1024), 0, s, nodes, lvl));
+}
+
+void launch_grind(Prof& prof, hipStream_t s, const uint32_t* seed_words, uint64_t base, uint64_t count,
+                  uint32_t bits, unsigned long long* result) {
+  SeedArg sa;
+  for (int i = 0; i < 8; i++) sa.w[i] = seed_words[i];
+  LAUNCH(prof, "grind", s,
+         hipLaunchKernelGGL(k_grind, dim3(blocks_for(count)), dim3(TPB), 0, s, sa, base, count, bits, result));
+}
+
+void launch_eval_mimc(Prof& prof, hipStream_t s, const EvalCommon& c, const MimcEvalArgs& a, const felt* lde,
+                      felt* comp) {
+  uint64_t M = 1ull << (c.logn + c.logce);
+  LAUNCH(prof, "eval_mimc", s,
+         hipLaunchKernelGGL(k_eval_mimc, dim3(blocks_for((M + EVAL_CH - 1) / EVAL_CH)), dim3(TPB), 0, s, c, a, lde,
+                            comp));
+}
+
+void launch_eval_linear(Prof& prof, hipStream_t s, const EvalCommon& c, const LinearEvalArgs& a, const felt* lde,
+                        felt* comp) {
+  uint64_t M = 1ull << (c.logn + c.logce);
+  LAUNCH(prof, "eval_linear", s,
+         hipLaunchKernelGGL(k_eval_linear, dim3(blocks_for((M + EVAL_CH - 1) / EVAL_CH)), dim3(TPB), 0, s, c, a, lde,
+                            comp));
+}
+
+void launch_segment(Prof& prof, hipStream_t s, const felt* difout, uint32_t logn, uint32_t logce, uint32_t C,
+                    const felt* Gi, const felt* scales, felt* out) {
+  LAUNCH(prof, "segment", s,
+         hipLaunchKernelGGL(k_segment, dim3(grid_stride_blocks((uint64_t)C << logn)), dim3(TPB), 0, s, difout, logn,
+                            logce, C, Gi, scales, out));
+}
+
+void launch_eval_bitrev(Prof& prof, hipStream_t s, const felt* arrays, uint32_t narrays, uint32_t logn,
+                        const felt* pw0, const felt* pw1, felt* partial, uint32_t* nblocks_out) {
+  uint32_t logE = logn < OOD_LOGE ? logn : OOD_LOGE;
+  uint32_t nb = 1u << (logn - logE);
+  *nblocks_out = nb;
+  LAUNCH(prof, "eval_bitrev", s,
+         hipLaunchKernelGGL(k_eval_bitrev, dim3(nb, narrays), dim3(TPB), 0, s, arrays, logn, logE, pw0, pw1,
+                            partial));
+}
+
+void launch_deep(Prof& prof, hipStream_t s, const DeepArgs& a, felt* out) {
+  uint64_t N = 1ull << a.logN;
+  LAUNCH(prof, "deep", s,
+         hipLaunchKernelGGL(k_deep, dim3(blocks_for((N + EVAL_CH - 1) / EVAL_CH)), dim3(TPB), 0, s, a, out));
+}
+
+void launch_fri_fold(Prof& prof, hipStream_t s, const felt* E, uint64_t R, uint32_t F, felt alpha, felt off_inv,
+                     const felt* itw, uint32_t logN, uint32_t logD, const felt* eps_inv, felt* out) {
+  (void)F;  // only 16 is compiled (the reference's fri_folding_factor)
+  uint32_t xsh = logN - logD;
+  LAUNCH(prof, "fri_fold16", s,
+         hipLaunchKernelGGL(k_fri_fold16, dim3(blocks_for(R)), dim3(TPB), 0, s, E, R, alpha, off_inv, itw, xsh,
+                            eps_inv, out));
+}
+
+void launch_gather_felts(Prof& prof, hipStream_t s, const felt* src, const uint64_t* idx, felt* out, uint64_t count) {
+  LAUNCH(prof, "gather", s,
+         hipLaunchKernelGGL(k_gather_felts, dim3(blocks_for(count)), dim3(TPB), 0, s, src, idx, out, count));
+}
+
+void launch_gather_digests(Prof& prof, hipStream_t s, const uint32_t* nodes, const uint64_t* idx, uint32_t* out,
+                           uint64_t count) {
+  LAUNCH(prof, "gather", s,
+         hipLaunchKernelGGL(k_gather_digests, dim3(blocks_for(count)), dim3(TPB), 0, s, nodes, idx, out, count));
+}

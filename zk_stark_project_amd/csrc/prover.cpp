@@ -1,0 +1,1092 @@
+// prover.cpp — host orchestration of the MI355X STARK prover + the C-ABI of
+// include/zkp.h.
+//
+// Mirrors winterfell 0.12 `Prover::generate_proof` (the path selected by the
+// reference's plug-ins, src/aggregation/prover.rs:194-248): channel seeding,
+// trace LDE + commitment, constraint evaluation, composition commitment, OOD,
+// DEEP, FRI, grinding, queries, serialization. Every O(n) stage runs on the
+// GPU (kernels.hip); the host only drives the Fiat-Shamir transcript and
+// assembles the proof bytes from the few values the verifier needs.
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <stdexcept>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "../../include/zkp.h"
+#include "blake3.hpp"
+#include "zkp_internal.hpp"
+
+using namespace fp;
+
+namespace {
+
+struct ZkpFail {
+  int code;
+  std::string msg;
+};
+
+#define HIP_CHECK(x)                                                                               \
+  do {                                                                                             \
+    hipError_t e_ = (x);                                                                           \
+    if (e_ != hipSuccess)                                                                          \
+      throw ZkpFail{e_ == hipErrorOutOfMemory ? ZKP_ERR_OOM : ZKP_ERR_DEVICE,                      \
+                    std::string(#x) + ": " + hipGetErrorString(e_)};                               \
+  } while (0)
+
+// ------------------------------------------------------------------ field helpers
+uint32_t ilog2(uint64_t v) {
+  uint32_t l = 0;
+  while ((1ull << l) < v) l++;
+  return l;
+}
+uint64_t revb(uint64_t x, uint32_t bits) {
+  uint64_t r = 0;
+  for (uint32_t i = 0; i < bits; i++) r |= ((x >> i) & 1ull) << (bits - 1 - i);
+  return r;
+}
+felt two_adic_root() { return make(0x86b8723e1920f4aaULL, 0x120532e7b364080aULL); }
+felt root_of_unity(uint32_t log_n) {
+  felt r = two_adic_root();
+  for (uint32_t i = log_n; i < 40; i++) r = sqr(r);
+  return r;
+}
+felt felt_u64(uint64_t v) { return make(v, 0); }
+
+// natural-order radix-2 NTT on the host (only for tiny arrays: remainder, periodic column)
+void host_ntt(std::vector<felt>& a, felt root) {
+  size_t n = a.size();
+  for (size_t i = 1, j = 0; i < n; i++) {
+    size_t bit = n >> 1;
+    for (; j & bit; bit >>= 1) j ^= bit;
+    j ^= bit;
+    if (i < j) std::swap(a[i], a[j]);
+  }
+  for (size_t len = 2; len <= n; len <<= 1) {
+    felt wl = pow_u64(root, n / len);
+    for (size_t i = 0; i < n; i += len) {
+      felt w = one();
+      for (size_t k = 0; k < len / 2; k++) {
+        felt u = a[i + k], v = mul(a[i + k + len / 2], w);
+        a[i + k] = add(u, v);
+        a[i + k + len / 2] = sub(u, v);
+        w = mul(w, wl);
+      }
+    }
+  }
+}
+// fft::interpolate_poly_with_offset
+void host_interpolate(std::vector<felt>& v, felt offset) {
+  size_t n = v.size();
+  host_ntt(v, inv(root_of_unity(ilog2(n))));
+  felt s = inv(felt_u64(n)), oi = inv(offset);
+  for (size_t k = 0; k < n; k++) { v[k] = mul(v[k], s); s = mul(s, oi); }
+}
+// fft::evaluate_poly_with_offset (coefficients zero-padded to N)
+std::vector<felt> host_evaluate(const std::vector<felt>& c, size_t N, felt offset) {
+  std::vector<felt> out(N, zero());
+  felt s = one();
+  for (size_t k = 0; k < c.size(); k++) { out[k] = mul(c[k], s); s = mul(s, offset); }
+  host_ntt(out, root_of_unity(ilog2(N)));
+  return out;
+}
+
+// ------------------------------------------------------------------ transcript
+void hash_elements(const felt* e, size_t n, uint8_t out[32]) {
+  std::vector<uint8_t> buf(n * 16);
+  for (size_t i = 0; i < n; i++) to_bytes(e[i], buf.data() + 16 * i);
+  b3::host_hash(buf.data(), buf.size(), out);
+}
+void merge_bytes(const uint8_t a[32], const uint8_t b[32], uint8_t out[32]) {
+  uint8_t buf[64];
+  memcpy(buf, a, 32);
+  memcpy(buf + 32, b, 32);
+  b3::host_hash(buf, 64, out);
+}
+void merge_with_int(const uint8_t s[32], uint64_t v, uint8_t out[32]) {
+  uint8_t buf[40];
+  memcpy(buf, s, 32);
+  for (int i = 0; i < 8; i++) buf[32 + i] = (uint8_t)(v >> (8 * i));
+  b3::host_hash(buf, 40, out);
+}
+
+// winter-crypto DefaultRandomCoin<Blake3_256>
+struct Coin {
+  uint8_t seed[32];
+  uint64_t counter = 0;
+  void init(const std::vector<felt>& els) { hash_elements(els.data(), els.size(), seed); counter = 0; }
+  void reseed(const uint8_t d[32]) {
+    uint8_t s[32];
+    merge_bytes(seed, d, s);
+    memcpy(seed, s, 32);
+    counter = 0;
+  }
+  void next(uint8_t out[32]) { counter++; merge_with_int(seed, counter, out); }
+  felt draw() {
+    for (int i = 0; i < 1000; i++) {
+      uint8_t v[32];
+      next(v);
+      felt x = from_u128_bytes(v);
+      if (!ge_p(x)) return x;
+    }
+    throw ZkpFail{ZKP_ERR_ARGUMENT, "failed to draw a field element"};
+  }
+  std::vector<uint64_t> draw_integers(uint32_t k, uint64_t domain, uint64_t nonce) {
+    uint8_t s[32];
+    merge_with_int(seed, nonce, s);
+    memcpy(seed, s, 32);
+    counter = 0;
+    std::vector<uint64_t> out(k);
+    for (uint32_t i = 0; i < k; i++) {
+      uint8_t v[32];
+      next(v);
+      uint64_t x = 0;
+      for (int b = 7; b >= 0; b--) x = (x << 8) | v[b];
+      out[i] = x & (domain - 1);
+    }
+    return out;
+  }
+};
+
+// ConstraintCompositionCoefficients / DeepCompositionCoefficients
+std::vector<felt> draw_coeffs(Coin& c, uint32_t method, uint32_t n) {
+  std::vector<felt> out(n);
+  if (method == ZKP_BATCHING_LINEAR) {
+    for (uint32_t i = 0; i < n; i++) out[i] = c.draw();
+    return out;
+  }
+  felt alpha = c.draw(), acc = one();
+  for (uint32_t i = 0; i < n; i++) {
+    out[method == ZKP_BATCHING_HORNER ? n - 1 - i : i] = acc;
+    acc = mul(acc, alpha);
+  }
+  return out;
+}
+
+// ------------------------------------------------------------------ serialization
+struct Writer {
+  std::vector<uint8_t> b;
+  void put(const void* p, size_t n) { b.insert(b.end(), (const uint8_t*)p, (const uint8_t*)p + n); }
+  void u8(uint8_t v) { b.push_back(v); }
+  void u16(uint16_t v) { u8((uint8_t)v); u8((uint8_t)(v >> 8)); }
+  void u32(uint32_t v) { for (int i = 0; i < 4; i++) u8((uint8_t)(v >> (8 * i))); }
+  void u64(uint64_t v) { for (int i = 0; i < 8; i++) u8((uint8_t)(v >> (8 * i))); }
+  void fe(felt v) { uint8_t t[16]; to_bytes(v, t); put(t, 16); }
+};
+
+// ------------------------------------------------------------------ AIR metadata
+constexpr uint32_t GU_D = 60;  // AC*FE + AC (src/helper.rs:18-20)
+
+struct AirDesc {
+  int id;
+  uint32_t w;
+  uint64_t n;
+  uint32_t num_t, base_degree, cycle;
+  std::vector<uint32_t> a_col;
+  std::vector<uint64_t> a_step;
+  std::vector<felt> a_val;
+  felt k;
+  uint32_t ce_blowup() const {
+    uint32_t v = base_degree - 1, p = 1;
+    while (p < v) p <<= 1;
+    return p < 2 ? 2 : p;
+  }
+  uint32_t comp_cols() const {
+    uint64_t hi = (uint64_t)base_degree * (n - 1), div = n - 1;
+    uint64_t c = (hi - div + n - 1) / n;
+    return c < 1 ? 1 : (uint32_t)c;
+  }
+};
+
+int build_air(AirDesc& a, int id, uint32_t w, uint64_t n, const std::vector<felt>& pub) {
+  a.id = id;
+  a.w = w;
+  a.n = n;
+  if (id == ZKP_AIR_MIMC) {
+    // builder-defined MiMC AIR, round constants src/helper.rs:404-406
+    if (w != 1 || n < 64 || pub.size() != 2) return ZKP_ERR_PUB_INPUTS;
+    a.num_t = 1;
+    a.base_degree = 7;
+    a.cycle = 64;
+    a.a_col = {0, 0};
+    a.a_step = {0, n - 1};
+    a.a_val = {pub[0], pub[1]};
+    return 0;
+  }
+  if (id == ZKP_AIR_GLOBAL_UPDATE) {
+    // src/aggregation/air.rs:93-147
+    if (w != 2 * GU_D || pub.size() != 123) return ZKP_ERR_PUB_INPUTS;
+    if (pub[122].hi != 0 || pub[122].lo == 0 || pub[122].lo > n) return ZKP_ERR_PUB_INPUTS;
+    uint64_t steps = pub[122].lo;
+    a.num_t = GU_D;
+    a.base_degree = 1;
+    a.cycle = 0;
+    a.k = pub[120];
+    for (uint32_t i = 0; i < 2 * GU_D; i++) {
+      a.a_col.push_back(i);
+      a.a_step.push_back(steps - 1);
+      a.a_val.push_back(i < GU_D ? pub[60 + i] : zero());
+    }
+    return 0;
+  }
+  return ZKP_ERR_UNSUPPORTED_AIR;
+}
+
+int check_options(const zkp_proof_options* o) {
+  if (!o) return ZKP_ERR_ARGUMENT;
+  if (o->field_extension != ZKP_FIELD_EXTENSION_NONE) return ZKP_ERR_UNSUPPORTED_FIELD_EXTENSION;
+  if (o->num_queries == 0 || o->num_queries > 255) return ZKP_ERR_INVALID_OPTIONS;
+  uint32_t b = o->blowup_factor;
+  if (b < 2 || b > 128 || (b & (b - 1))) return ZKP_ERR_INVALID_OPTIONS;
+  if (o->grinding_factor > 32) return ZKP_ERR_INVALID_OPTIONS;
+  if (o->fri_folding_factor != 16) return ZKP_ERR_INVALID_OPTIONS;  // the reference's value; only 16 is built
+  uint32_t r = o->fri_remainder_max_degree;
+  if (r > 255 || ((r + 1) & r)) return ZKP_ERR_INVALID_OPTIONS;
+  if (o->batching_constraints > 2 || o->batching_deep > 2) return ZKP_ERR_INVALID_OPTIONS;
+  return 0;
+}
+
+// Context::to_elements
+std::vector<felt> context_elements(const AirDesc& a, const zkp_proof_options* o) {
+  std::vector<felt> e;
+  e.push_back(felt_u64((uint64_t)a.w << 16));
+  e.push_back(felt_u64((uint32_t)a.n));
+  e.push_back(felt_u64(0xffffd30000000001ULL));
+  e.push_back(felt_u64(0xffffffffffffffffULL));
+  e.push_back(felt_u64(a.num_t + a.a_col.size()));
+  uint32_t buf = o->field_extension;
+  buf = (buf << 8) | o->fri_folding_factor;
+  buf = (buf << 8) | o->fri_remainder_max_degree;
+  buf = (buf << 8) | o->blowup_factor;
+  e.push_back(felt_u64(buf));
+  e.push_back(felt_u64(o->grinding_factor));
+  e.push_back(felt_u64(o->num_queries));
+  return e;
+}
+
+void write_context(Writer& w, const AirDesc& a, const zkp_proof_options* o) {
+  w.u8((uint8_t)a.w); w.u8(0); w.u8(0); w.u8((uint8_t)ilog2(a.n)); w.u16(0);
+  w.u8(16); w.fe(make(P_LO, P_HI));
+  w.u8((uint8_t)o->num_queries); w.u8((uint8_t)o->blowup_factor); w.u8((uint8_t)o->grinding_factor);
+  w.u8((uint8_t)o->field_extension); w.u8((uint8_t)o->fri_folding_factor); w.u8((uint8_t)o->fri_remainder_max_degree);
+  w.u8((uint8_t)o->batching_constraints); w.u8((uint8_t)o->batching_deep);
+  w.u32((uint32_t)(a.num_t + a.a_col.size()));
+}
+
+// MerkleTree::prove_batch plan: emission order of (path slot, node index).
+// Node numbering: leaves at L + i, internal nodes 1..L-1 (same as the device tree).
+struct BatchPlan {
+  uint32_t depth;
+  std::vector<std::vector<uint64_t>> paths;  // node indices per path
+};
+BatchPlan plan_batch(uint64_t L, const std::vector<uint64_t>& idx) {
+  BatchPlan bp;
+  bp.depth = ilog2(L);
+  std::vector<uint64_t> norm;
+  for (uint64_t i : idx) norm.push_back(i & ~1ull);
+  std::sort(norm.begin(), norm.end());
+  norm.erase(std::unique(norm.begin(), norm.end()), norm.end());
+  auto has = [&](uint64_t v) { return std::find(idx.begin(), idx.end(), v) != idx.end(); };
+  bp.paths.resize(norm.size());
+  std::vector<uint64_t> next, cur;
+  for (size_t i = 0; i < norm.size(); i++) {
+    uint64_t a = norm[i];
+    bool ha = has(a), hb = has(a + 1);
+    if (ha && !hb) bp.paths[i].push_back(L + a + 1);
+    else if (!ha) bp.paths[i].push_back(L + a);
+    next.push_back((a + L) >> 1);
+  }
+  for (uint32_t d = 1; d < bp.depth; d++) {
+    cur = next;
+    next.clear();
+    for (size_t i = 0; i < cur.size(); i++) {
+      uint64_t node = cur[i], sib = node ^ 1;
+      if (i + 1 < cur.size() && cur[i + 1] == sib) i++;
+      else bp.paths[i].push_back(sib);
+      next.push_back(sib >> 1);
+    }
+  }
+  return bp;
+}
+
+std::vector<uint64_t> fold_positions(const std::vector<uint64_t>& pos, uint64_t target) {
+  std::vector<uint64_t> out;
+  for (uint64_t p : pos) {
+    uint64_t q = p % target;
+    if (std::find(out.begin(), out.end(), q) == out.end()) out.push_back(q);
+  }
+  return out;
+}
+
+}  // namespace
+
+// ====================================================================== context
+struct DevBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+};
+
+struct zkp_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  Prof prof;
+  std::string err;
+  std::map<std::string, DevBuf> bufs;
+  std::map<std::string, std::pair<uint64_t, double>> stats;
+  std::vector<void*> user_allocs;
+
+  template <typename T>
+  T* buf(const std::string& name, size_t count) {
+    size_t bytes = count * sizeof(T);
+    if (bytes == 0) bytes = 16;
+    DevBuf& b = bufs[name];
+    if (b.bytes < bytes) {
+      if (b.p) HIP_CHECK(hipFree(b.p));
+      b.p = nullptr;
+      HIP_CHECK(hipMalloc(&b.p, bytes));
+      b.bytes = bytes;
+    }
+    return reinterpret_cast<T*>(b.p);
+  }
+  void sync() { HIP_CHECK(hipStreamSynchronize(stream)); }
+  void upload(void* d, const void* h, size_t bytes) {
+    HIP_CHECK(hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, stream));
+  }
+  void download(void* h, const void* d, size_t bytes) {
+    HIP_CHECK(hipMemcpyAsync(h, d, bytes, hipMemcpyDeviceToHost, stream));
+    sync();
+  }
+  void collect_prof() {
+    if (prof.pending.empty()) return;
+    sync();
+    for (auto& r : prof.pending) {
+      float ms = 0;
+      HIP_CHECK(hipEventElapsedTime(&ms, r.start, r.stop));
+      auto& s = stats[r.name];
+      s.first += 1;
+      s.second += ms;
+      prof.pool.push_back(r.start);
+      prof.pool.push_back(r.stop);
+    }
+    prof.pending.clear();
+  }
+
+  // ---- twiddle tables for domain 2^logN: tw[e] = w^e, itw[e] = w^-e (e < N/2)
+  std::map<uint32_t, bool> have_tw;
+  void ensure_twiddles(uint32_t logN) {
+    if (have_tw[logN]) return;
+    uint64_t half = 1ull << (logN - 1);
+    for (int dir = 0; dir < 2; dir++) {
+      felt w = root_of_unity(logN);
+      if (dir) w = inv(w);
+      std::vector<felt> lo(2048), hi((half + 2047) / 2048 + 1);
+      lo[0] = one();
+      for (int i = 1; i < 2048; i++) lo[i] = mul(lo[i - 1], w);
+      felt step = mul(lo[2047], w);
+      hi[0] = one();
+      for (size_t i = 1; i < hi.size(); i++) hi[i] = mul(hi[i - 1], step);
+      felt* dlo = buf<felt>("tmp_lo", lo.size());
+      felt* dhi = buf<felt>("tmp_hi", hi.size());
+      upload(dlo, lo.data(), lo.size() * 16);
+      upload(dhi, hi.data(), hi.size() * 16);
+      felt* t = buf<felt>((dir ? "itw_" : "tw_") + std::to_string(logN), half);
+      launch_expand_powers(prof, stream, t, half, dlo, dhi);
+      sync();
+    }
+    have_tw[logN] = true;
+  }
+  felt* tw(uint32_t logN) { return reinterpret_cast<felt*>(bufs["tw_" + std::to_string(logN)].p); }
+  felt* itw(uint32_t logN) { return reinterpret_cast<felt*>(bufs["itw_" + std::to_string(logN)].p); }
+
+  // ---- coset tables for (n, B): S[j*n + p] = n^-1 (g w_N^j)^rev(p) ; Gi[p] = g^-rev(p)
+  std::map<std::pair<uint32_t, uint32_t>, bool> have_coset;
+  void ensure_coset(uint32_t logn, uint32_t logB) {
+    auto key = std::make_pair(logn, logB);
+    if (have_coset[key]) return;
+    uint32_t logN = logn + logB;
+    ensure_twiddles(logN);
+    uint64_t n = 1ull << logn;
+    felt g = felt_u64(3);
+    for (int dir = 0; dir < 2; dir++) {
+      felt base = dir ? inv(g) : g;
+      std::vector<felt> lo(2048), hi(n / 2048 + 2);
+      lo[0] = one();
+      for (int i = 1; i < 2048; i++) lo[i] = mul(lo[i - 1], base);
+      felt step = mul(lo[2047], base);
+      hi[0] = one();
+      for (size_t i = 1; i < hi.size(); i++) hi[i] = mul(hi[i - 1], step);
+      felt* dlo = buf<felt>("tmp_lo", lo.size());
+      felt* dhi = buf<felt>("tmp_hi", hi.size());
+      upload(dlo, lo.data(), lo.size() * 16);
+      upload(dhi, hi.data(), hi.size() * 16);
+      std::string sfx = std::to_string(logn) + "_" + std::to_string(logB);
+      if (dir == 0) {
+        felt* S = buf<felt>("S_" + sfx, n << logB);
+        launch_build_coset_scale(prof, stream, S, logn, 1u << logB, tw(logN), logN, dlo, dhi, inv(felt_u64(n)));
+      } else {
+        felt* Gi = buf<felt>("Gi_" + sfx, n);
+        launch_build_ginv(prof, stream, Gi, logn, dlo, dhi);
+      }
+      sync();
+    }
+    have_coset[key] = true;
+  }
+  felt* S(uint32_t logn, uint32_t logB) {
+    return reinterpret_cast<felt*>(bufs["S_" + std::to_string(logn) + "_" + std::to_string(logB)].p);
+  }
+  felt* Gi(uint32_t logn, uint32_t logB) {
+    return reinterpret_cast<felt*>(bufs["Gi_" + std::to_string(logn) + "_" + std::to_string(logB)].p);
+  }
+
+  ~zkp_ctx() {
+    for (auto& kv : bufs)
+      if (kv.second.p) (void)hipFree(kv.second.p);
+    for (void* p : user_allocs) (void)hipFree(p);
+    for (auto e : prof.pool) (void)hipEventDestroy(e);
+    if (stream) (void)hipStreamDestroy(stream);
+  }
+};
+
+namespace {
+
+// ------------------------------------------------------------------ stage: LDE + commit
+// d_in (w x n natural) -> tcoef (w x n, bitrev, scaled by n), lde (w x B x n coset-major),
+// tree nodes (2N digests) ; returns root
+void lde_commit(zkp_ctx* ctx, const felt* d_in, uint32_t w, uint32_t logn, uint32_t logB, felt* coef, felt* lde,
+                uint32_t* nodes, bool input_is_coef, uint8_t root[32]) {
+  uint32_t logN = logn + logB;
+  uint64_t n = 1ull << logn, N = 1ull << logN;
+  ctx->ensure_coset(logn, logB);
+  if (!input_is_coef) {
+    NttBatch ib{d_in, coef, nullptr, n, n, 1, 1, w};
+    launch_ntt(ctx->prof, ctx->stream, ib, logn, false, ctx->itw(logN), logN);
+  }
+  NttBatch lb{coef, lde, ctx->S(logn, logB), n, n, 1u << logB, 1u << logB, w << logB};
+  launch_ntt(ctx->prof, ctx->stream, lb, logn, true, ctx->tw(logN), logN);
+  launch_leaf_hash_lde(ctx->prof, ctx->stream, lde, w, logB, n, nodes, N);
+  launch_merkle_tree(ctx->prof, ctx->stream, nodes, N);
+  ctx->download(root, nodes + 8, 32);
+}
+
+// evaluate bit-reversed coefficient arrays (scaled by n) at x0, x1 -> values (x n^-1)
+void ood_eval(zkp_ctx* ctx, const felt* arrays, uint32_t narrays, uint32_t logn, felt x0, felt x1,
+              std::vector<felt>& v0, std::vector<felt>& v1) {
+  std::vector<felt> pw0(logn), pw1(logn);
+  felt a = x0, b = x1;
+  for (uint32_t l = 0; l < logn; l++) { pw0[l] = a; pw1[l] = b; a = sqr(a); b = sqr(b); }
+  felt* dpw = ctx->buf<felt>("ood_pw", 2 * (logn + 1));
+  ctx->upload(dpw, pw0.data(), logn * 16);
+  ctx->upload(dpw + logn, pw1.data(), logn * 16);
+  uint32_t nb = 0;
+  uint32_t logE = logn < 11 ? logn : 11;
+  felt* part = ctx->buf<felt>("ood_part", (size_t)2 * narrays * (1ull << (logn - logE)));
+  launch_eval_bitrev(ctx->prof, ctx->stream, arrays, narrays, logn, dpw, dpw + logn, part, &nb);
+  std::vector<felt> hp((size_t)2 * narrays * nb);
+  ctx->download(hp.data(), part, hp.size() * 16);
+  felt ninv = inv(felt_u64(1ull << logn));
+  v0.assign(narrays, zero());
+  v1.assign(narrays, zero());
+  for (uint32_t arr = 0; arr < narrays; arr++) {
+    for (int k = 0; k < 2; k++) {
+      std::vector<felt> cur(nb);
+      for (uint32_t b2 = 0; b2 < nb; b2++) cur[b2] = hp[((size_t)arr * nb + b2) * 2 + k];
+      const std::vector<felt>& pw = k ? pw1 : pw0;
+      uint32_t l = logE;
+      while (cur.size() > 1) {
+        std::vector<felt> nx(cur.size() / 2);
+        for (size_t i = 0; i < nx.size(); i++) nx[i] = add(cur[2 * i], mul(pw[logn - 1 - l], cur[2 * i + 1]));
+        cur.swap(nx);
+        l++;
+      }
+      (k ? v1 : v0)[arr] = mul(cur[0], ninv);
+    }
+  }
+}
+
+int prove_impl(zkp_ctx* ctx, int air_id, const felt* d_trace, uint32_t w, uint64_t n, const zkp_felt* pub_elems,
+               uint64_t n_pub, const zkp_proof_options* o, uint8_t** proof, uint64_t* proof_len,
+               zkp_transcript* tr_out) {
+  int rc = check_options(o);
+  if (rc) return rc;
+  if (n < 8 || (n & (n - 1)) || w == 0 || w > 255) return ZKP_ERR_TRACE_SHAPE;
+  if (!proof || !proof_len || (n_pub && !pub_elems)) return ZKP_ERR_ARGUMENT;
+  const uint32_t B = o->blowup_factor, F = o->fri_folding_factor;
+  const uint32_t logn = ilog2(n), logB = ilog2(B), logN = logn + logB;
+  const uint64_t N = 1ull << logN;
+  if (logN > 32) return ZKP_ERR_TRACE_SHAPE;
+  std::vector<felt> pub(n_pub);
+  for (uint64_t i = 0; i < n_pub; i++) pub[i] = make(pub_elems[i].lo, pub_elems[i].hi);
+  AirDesc air;
+  rc = build_air(air, air_id, w, n, pub);
+  if (rc) return rc;
+  const uint32_t ce = air.ce_blowup(), C = air.comp_cols();
+  if (B < ce) return ZKP_ERR_INVALID_OPTIONS;
+  const uint32_t logce = ilog2(ce);
+  const uint64_t M = n * ce;
+  const felt g = felt_u64(3);
+  zkp_transcript T;
+  memset(&T, 0, sizeof T);
+  hipStream_t st = ctx->stream;
+  Prof& pf = ctx->prof;
+
+  // 1. channel: Context::to_elements || pub_inputs.to_elements
+  Coin coin;
+  {
+    std::vector<felt> se = context_elements(air, o);
+    se.insert(se.end(), pub.begin(), pub.end());
+    coin.init(se);
+  }
+  ctx->ensure_coset(logn, logB);
+
+  // 2. trace LDE + commitment (DefaultTraceLde::new)
+  felt* coef = ctx->buf<felt>("coef", (size_t)(w + C) * n);
+  felt* tlde = ctx->buf<felt>("tlde", (size_t)w * N);
+  uint32_t* ttree = ctx->buf<uint32_t>("ttree", (size_t)16 * N);
+  lde_commit(ctx, d_trace, w, logn, logB, coef, tlde, ttree, false, T.trace_root);
+  coin.reseed(T.trace_root);
+
+  // 3. constraint composition coefficients + evaluation (DefaultConstraintEvaluator)
+  const uint32_t ncoef = air.num_t + (uint32_t)air.a_col.size();
+  std::vector<felt> cc = draw_coeffs(coin, o->batching_constraints, ncoef);
+  felt* comp = ctx->buf<felt>("comp", M);
+  {
+    felt wn = root_of_unity(logn);
+    EvalCommon ec;
+    ec.logn = logn; ec.logB = logB; ec.logce = logce; ec.logN = logN;
+    ec.g = g;
+    ec.w_last = pow_u64(wn, n - 1);
+    ec.tw = ctx->tw(logN);
+    // 1/(x^n - 1) on the CE domain: x^n = g^n * w_ce^s
+    std::vector<felt> zinv(ce);
+    felt gn = pow_u64(g, n), wce = root_of_unity(logce);
+    for (uint32_t s = 0; s < ce; s++) zinv[s] = inv(sub(mul(gn, pow_u64(wce, s)), one()));
+    felt* dz = ctx->buf<felt>("zinv", ce);
+    ctx->upload(dz, zinv.data(), ce * 16);
+    ec.zinv = dz;
+    if (air.id == ZKP_AIR_MIMC) {
+      // periodic column K over the CE domain: interpolate over <w_64>, evaluate at g^(n/64) * <w_{64 ce}>
+      std::vector<felt> kc(64);
+      for (int j = 0; j < 64; j++) kc[j] = felt_u64((uint64_t)(j + 1) * 1000000ull);
+      host_interpolate(kc, one());
+      std::vector<felt> kv = host_evaluate(kc, 64 * ce, pow_u64(g, n / 64));
+      felt* dk = ctx->buf<felt>("kper", kv.size());
+      ctx->upload(dk, kv.data(), kv.size() * 16);
+      MimcEvalArgs ma;
+      ma.coef_t = cc[0];
+      ma.b0 = cc[1]; ma.v0 = air.a_val[0];
+      ma.b1 = cc[2]; ma.v1 = air.a_val[1];
+      ma.kper = dk;
+      launch_eval_mimc(pf, st, ec, ma, tlde, comp);
+    } else {
+      // GlobalUpdate: T = sum_i a^i (k*next_i - k*cur_i - next_{i+60}); B = sum_c b_c (cur_c - v_c)
+      std::vector<felt> co(3 * w, zero());
+      for (uint32_t i = 0; i < GU_D; i++) {
+        co[i] = mul(cc[i], air.k);                    // next_i
+        co[w + i] = neg(mul(cc[i], air.k));           // cur_i
+        co[i + GU_D] = neg(cc[i]);                    // next_{i+60}
+      }
+      felt bconst = zero();
+      for (uint32_t c = 0; c < w; c++) {
+        co[2 * w + c] = cc[air.num_t + c];
+        bconst = add(bconst, mul(cc[air.num_t + c], air.a_val[c]));
+      }
+      felt* dco = ctx->buf<felt>("lin_coefs", co.size());
+      ctx->upload(dco, co.data(), co.size() * 16);
+      LinearEvalArgs la;
+      la.width = w;
+      la.coefs = dco;
+      la.bconst = bconst;
+      la.w_bstep = pow_u64(wn, air.a_step[0]);
+      launch_eval_linear(pf, st, ec, la, tlde, comp);
+    }
+  }
+
+  // 4. composition polynomial + commitment (DefaultConstraintCommitment)
+  felt* acoef = coef + (size_t)w * n;
+  felt* clde = ctx->buf<felt>("clde", (size_t)C * N);
+  uint32_t* ctree = ctx->buf<uint32_t>("ctree", (size_t)16 * N);
+  {
+    NttBatch ib{comp, comp, nullptr, M, M, 1, 1, 1};
+    launch_ntt(pf, st, ib, logn + logce, false, ctx->itw(logN), logN);
+    std::vector<felt> sc(C);
+    felt nm = mul(felt_u64(n), inv(felt_u64(M)));
+    felt ginv_n = inv(pow_u64(g, n));
+    felt acc = nm;
+    for (uint32_t h = 0; h < C; h++) { sc[h] = acc; acc = mul(acc, ginv_n); }
+    felt* dsc = ctx->buf<felt>("seg_scales", C);
+    ctx->upload(dsc, sc.data(), C * 16);
+    launch_segment(pf, st, comp, logn, logce, C, ctx->Gi(logn, logB), dsc, acoef);
+    lde_commit(ctx, nullptr, C, logn, logB, acoef, clde, ctree, true, T.constraint_root);
+  }
+  coin.reseed(T.constraint_root);
+
+  // 5. OOD frame
+  felt z = coin.draw();
+  T.z.lo = z.lo; T.z.hi = z.hi;
+  felt zg = mul(z, root_of_unity(logn));
+  std::vector<felt> oz, ozg;
+  ood_eval(ctx, coef, w + C, logn, z, zg, oz, ozg);
+  std::vector<felt> ood_trace(2 * w);
+  for (uint32_t c = 0; c < w; c++) { ood_trace[c] = oz[c]; ood_trace[w + c] = ozg[c]; }
+  std::vector<felt> ood_comp(oz.begin() + w, oz.end());
+  uint8_t dg[32];
+  hash_elements(ood_trace.data(), ood_trace.size(), dg);
+  coin.reseed(dg);
+  hash_elements(ood_comp.data(), ood_comp.size(), dg);
+  coin.reseed(dg);
+
+  // 6. DEEP composition evaluations over the LDE domain
+  std::vector<felt> gam = draw_coeffs(coin, o->batching_deep, w + C);
+  felt* deep = ctx->buf<felt>("deep", N);
+  {
+    felt kz = zero(), kzg = zero();
+    for (uint32_t c = 0; c < w; c++) { kz = add(kz, mul(gam[c], oz[c])); kzg = add(kzg, mul(gam[c], ozg[c])); }
+    for (uint32_t h = 0; h < C; h++) kz = add(kz, mul(gam[w + h], oz[w + h]));
+    felt* dg2 = ctx->buf<felt>("gamma", w + C);
+    ctx->upload(dg2, gam.data(), gam.size() * 16);
+    DeepArgs da;
+    da.w = w; da.C = C; da.logB = logB; da.logn = logn; da.logN = logN;
+    da.tlde = tlde; da.clde = clde; da.gamma = dg2;
+    da.z = z; da.zg = zg; da.kz = kz; da.kzg = kzg; da.g = g;
+    da.tw = ctx->tw(logN);
+    launch_deep(pf, st, da, deep);
+  }
+
+  // 7. FRI layers (FriProver::build_layers), folding factor 16
+  uint32_t L = 0;
+  {
+    uint64_t D = N, maxrem = (uint64_t)(o->fri_remainder_max_degree + 1) * B;
+    while (D > maxrem) { D /= F; L++; }
+  }
+  std::vector<felt> remainder;
+  std::vector<felt*> layer_evals(L + 1);
+  std::vector<uint32_t*> layer_trees(L);
+  std::vector<uint64_t> layer_size(L + 1);
+  {
+    // all later layers in one buffer; trees in one buffer
+    uint64_t tot_e = 0, tot_t = 0, D = N;
+    for (uint32_t l = 0; l < L; l++) { tot_e += D / F; tot_t += 2 * (D / F); D /= F; }
+    felt* fe = ctx->buf<felt>("fri_evals", tot_e + 1);
+    uint32_t* ft = ctx->buf<uint32_t>("fri_trees", 8 * (tot_t + 1));
+    std::vector<felt> eps(9);
+    felt einv = inv(root_of_unity(4));
+    eps[0] = one();
+    for (int m = 1; m < 8; m++) eps[m] = mul(eps[m - 1], einv);
+    eps[8] = inv(felt_u64(16));
+    felt* deps = ctx->buf<felt>("eps_inv", 9);
+    ctx->upload(deps, eps.data(), 9 * 16);
+    layer_evals[0] = deep;
+    D = N;
+    felt off = g;
+    uint64_t eo = 0, to = 0;
+    for (uint32_t l = 0; l < L; l++) {
+      uint64_t R = D / F;
+      layer_size[l] = D;
+      uint32_t* nodes = ft + 8 * to;
+      layer_trees[l] = nodes;
+      launch_leaf_hash_fri(pf, st, layer_evals[l], R, F, nodes);
+      launch_merkle_tree(pf, st, nodes, R);
+      ctx->download(T.fri_roots[l], nodes + 8, 32);
+      coin.reseed(T.fri_roots[l]);
+      felt alpha = coin.draw();
+      felt* nxt = fe + eo;
+      launch_fri_fold(pf, st, layer_evals[l], R, F, alpha, inv(off), ctx->itw(logN), logN, ilog2(D), deps, nxt);
+      layer_evals[l + 1] = nxt;
+      eo += R;
+      to += 2 * R;
+      D = R;
+      off = pow_u64(off, F);
+    }
+    layer_size[L] = D;
+    // remainder polynomial (FriProver::set_remainder): interpolate the last layer, keep D/B coefficients
+    remainder.resize(D);
+    ctx->download(remainder.data(), layer_evals[L], D * 16);
+    host_interpolate(remainder, off);
+    remainder.resize(D / B);
+    hash_elements(remainder.data(), remainder.size(), T.remainder_commitment);
+    coin.reseed(T.remainder_commitment);
+    T.num_fri_layers = L;
+  }
+
+  // 8. grinding: minimum nonce >= 1
+  uint64_t nonce = 0;
+  if (o->grinding_factor == 0) {
+    nonce = 1;
+  } else {
+    unsigned long long* dres = ctx->buf<unsigned long long>("grind_res", 1);
+    uint32_t sw[8];
+    for (int i = 0; i < 8; i++)
+      sw[i] = (uint32_t)coin.seed[4 * i] | ((uint32_t)coin.seed[4 * i + 1] << 8) |
+              ((uint32_t)coin.seed[4 * i + 2] << 16) | ((uint32_t)coin.seed[4 * i + 3] << 24);
+    const uint64_t chunk = 1ull << 22;
+    for (uint64_t base = 1; nonce == 0; base += chunk) {
+      unsigned long long init = ~0ull;
+      ctx->upload(dres, &init, 8);
+      launch_grind(pf, st, sw, base, chunk, o->grinding_factor, dres);
+      unsigned long long res;
+      ctx->download(&res, dres, 8);
+      if (res != ~0ull) nonce = res;
+      if (base > (1ull << 40)) throw ZkpFail{ZKP_ERR_NONCE, "nonce not found"};
+    }
+  }
+  T.pow_nonce = nonce;
+
+  // 9. query positions
+  std::vector<uint64_t> pos = coin.draw_integers(o->num_queries, N, nonce);
+  std::sort(pos.begin(), pos.end());
+  pos.erase(std::unique(pos.begin(), pos.end()), pos.end());
+  const uint64_t np = pos.size();
+  T.num_unique_queries = (uint32_t)np;
+  for (uint64_t i = 0; i < np; i++) T.query_positions[i] = pos[i];
+  T.num_composition_columns = C;
+
+  // gather all opened values and Merkle nodes
+  std::vector<uint64_t> fidx_t, fidx_c;
+  for (uint64_t p : pos) {
+    uint64_t j = p & (B - 1), t = p >> logB;
+    for (uint32_t c = 0; c < w; c++) fidx_t.push_back(((uint64_t)c * B + j) * n + t);
+    for (uint32_t h = 0; h < C; h++) fidx_c.push_back(((uint64_t)h * B + j) * n + t);
+  }
+  BatchPlan bt = plan_batch(N, pos), bc = plan_batch(N, pos);
+  std::vector<std::vector<uint64_t>> fpos(L);
+  std::vector<BatchPlan> bf(L);
+  std::vector<std::vector<uint64_t>> fidx(L);
+  {
+    std::vector<uint64_t> cur = pos;
+    for (uint32_t l = 0; l < L; l++) {
+      uint64_t R = layer_size[l] / F;
+      fpos[l] = fold_positions(cur, R);
+      bf[l] = plan_batch(R, fpos[l]);
+      for (uint64_t r : fpos[l])
+        for (uint32_t k = 0; k < F; k++) fidx[l].push_back(r + k * R);
+      cur = fpos[l];
+    }
+  }
+  auto gather_f = [&](const felt* src, const std::vector<uint64_t>& idx) {
+    std::vector<felt> out(idx.size());
+    if (idx.empty()) return out;
+    uint64_t* di = ctx->buf<uint64_t>("gidx", idx.size());
+    felt* dout = ctx->buf<felt>("gout", idx.size());
+    ctx->upload(di, idx.data(), idx.size() * 8);
+    launch_gather_felts(pf, st, src, di, dout, idx.size());
+    ctx->download(out.data(), dout, out.size() * 16);
+    return out;
+  };
+  auto gather_d = [&](const uint32_t* nodes, const BatchPlan& bp) {
+    std::vector<uint64_t> idx;
+    for (auto& p : bp.paths) idx.insert(idx.end(), p.begin(), p.end());
+    std::vector<uint32_t> out(idx.size() * 8);
+    if (idx.empty()) return out;
+    uint64_t* di = ctx->buf<uint64_t>("gidx", idx.size());
+    uint32_t* dout = ctx->buf<uint32_t>("gdout", idx.size() * 8);
+    ctx->upload(di, idx.data(), idx.size() * 8);
+    launch_gather_digests(pf, st, nodes, di, dout, idx.size());
+    ctx->download(out.data(), dout, out.size() * 4);
+    return out;
+  };
+  auto write_batch = [&](Writer& wr, const BatchPlan& bp, const std::vector<uint32_t>& d) {
+    wr.u8((uint8_t)bp.depth);
+    wr.u8((uint8_t)bp.paths.size());
+    size_t k = 0;
+    for (auto& p : bp.paths) {
+      wr.u8((uint8_t)p.size());
+      for (size_t i = 0; i < p.size(); i++, k++) wr.put(d.data() + 8 * k, 32);
+    }
+  };
+
+  // 10. serialize (≙ Proof::to_bytes)
+  Writer wr;
+  write_context(wr, air, o);
+  wr.u8((uint8_t)np);
+  wr.u16((uint16_t)(32 * (2 + L + 1)));
+  wr.put(T.trace_root, 32);
+  wr.put(T.constraint_root, 32);
+  for (uint32_t l = 0; l < L; l++) wr.put(T.fri_roots[l], 32);
+  wr.put(T.remainder_commitment, 32);
+  wr.u8(1);
+  for (int seg = 0; seg < 2; seg++) {
+    std::vector<felt> vals = gather_f(seg == 0 ? tlde : clde, seg == 0 ? fidx_t : fidx_c);
+    std::vector<uint32_t> dig = gather_d(seg == 0 ? ttree : ctree, seg == 0 ? bt : bc);
+    Writer vw, pw;
+    for (felt v : vals) vw.fe(v);
+    write_batch(pw, seg == 0 ? bt : bc, dig);
+    wr.u32((uint32_t)vw.b.size()); wr.put(vw.b.data(), vw.b.size());
+    wr.u32((uint32_t)pw.b.size()); wr.put(pw.b.data(), pw.b.size());
+  }
+  wr.u16((uint16_t)(1 + 16 * 2 * w));
+  wr.u8(2);
+  for (felt v : ood_trace) wr.fe(v);
+  wr.u16((uint16_t)(16 * C));
+  for (felt v : ood_comp) wr.fe(v);
+  wr.u8((uint8_t)L);
+  for (uint32_t l = 0; l < L; l++) {
+    std::vector<felt> vals = gather_f(layer_evals[l], fidx[l]);
+    std::vector<uint32_t> dig = gather_d(layer_trees[l], bf[l]);
+    Writer vw, pw;
+    for (felt v : vals) vw.fe(v);
+    write_batch(pw, bf[l], dig);
+    wr.u32((uint32_t)vw.b.size()); wr.put(vw.b.data(), vw.b.size());
+    wr.u32((uint32_t)pw.b.size()); wr.put(pw.b.data(), pw.b.size());
+  }
+  wr.u16((uint16_t)(16 * remainder.size()));
+  for (felt v : remainder) wr.fe(v);
+  wr.u8(1);
+  wr.u64(nonce);
+  wr.u8(0);
+
+  ctx->collect_prof();
+  uint8_t* out = (uint8_t*)malloc(wr.b.size());
+  if (!out) return ZKP_ERR_OOM;
+  memcpy(out, wr.b.data(), wr.b.size());
+  *proof = out;
+  *proof_len = wr.b.size();
+  if (tr_out) *tr_out = T;
+  return 0;
+}
+
+template <typename F>
+int guarded(zkp_ctx* ctx, F&& f) {
+  if (!ctx) return ZKP_ERR_ARGUMENT;
+  try {
+    int rc = f();
+    if (rc && ctx->err.empty()) ctx->err = "status " + std::to_string(rc);
+    return rc;
+  } catch (const ZkpFail& e) {
+    ctx->err = e.msg;
+    ctx->prof.pending.clear();
+    return e.code;
+  } catch (const std::bad_alloc&) {
+    ctx->err = "host out of memory";
+    return ZKP_ERR_OOM;
+  } catch (...) {
+    ctx->err = "unknown failure";
+    return ZKP_ERR_DEVICE;
+  }
+}
+
+}  // namespace
+
+// ====================================================================== C-ABI
+extern "C" {
+
+int zkp_ctx_create(int device, zkp_ctx** out) {
+  if (!out) return ZKP_ERR_ARGUMENT;
+  *out = nullptr;
+  int count = 0;
+  if (hipGetDeviceCount(&count) != hipSuccess || count <= device || device < 0) return ZKP_ERR_DEVICE;
+  if (hipSetDevice(device) != hipSuccess) return ZKP_ERR_DEVICE;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) != hipSuccess) return ZKP_ERR_DEVICE;
+  if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) return ZKP_ERR_DEVICE;  // code objects are gfx950-only
+  zkp_ctx* c = new (std::nothrow) zkp_ctx();
+  if (!c) return ZKP_ERR_OOM;
+  c->device = device;
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete c;
+    return ZKP_ERR_DEVICE;
+  }
+  *out = c;
+  return ZKP_OK;
+}
+
+void zkp_ctx_destroy(zkp_ctx* ctx) {
+  if (!ctx) return;
+  (void)hipSetDevice(ctx->device);
+  (void)hipStreamSynchronize(ctx->stream);
+  delete ctx;
+}
+
+const char* zkp_last_error(const zkp_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+void zkp_free(void* p) { free(p); }
+
+int zkp_prove_device(zkp_ctx* ctx, zkp_air_id air, const void* d_trace, uint32_t width, uint64_t n,
+                     const zkp_felt* pub, uint64_t n_pub, const zkp_proof_options* opts, uint8_t** proof,
+                     uint64_t* proof_len, zkp_transcript* transcript) {
+  return guarded(ctx, [&] {
+    ctx->err.clear();
+    HIP_CHECK(hipSetDevice(ctx->device));
+    if (!d_trace) return (int)ZKP_ERR_ARGUMENT;
+    return prove_impl(ctx, air, (const felt*)d_trace, width, n, pub, n_pub, opts, proof, proof_len, transcript);
+  });
+}
+
+int zkp_prove(zkp_ctx* ctx, zkp_air_id air, const zkp_felt* trace, uint32_t width, uint64_t n, const zkp_felt* pub,
+              uint64_t n_pub, const zkp_proof_options* opts, uint8_t** proof, uint64_t* proof_len,
+              zkp_transcript* transcript) {
+  return guarded(ctx, [&] {
+    ctx->err.clear();
+    HIP_CHECK(hipSetDevice(ctx->device));
+    if (!trace) return (int)ZKP_ERR_ARGUMENT;
+    if (n < 8 || (n & (n - 1)) || width == 0 || width > 255) return (int)ZKP_ERR_TRACE_SHAPE;
+    felt* d = ctx->buf<felt>("trace_in", (size_t)width * n);
+    ctx->upload(d, trace, (size_t)width * n * 16);
+    return prove_impl(ctx, air, d, width, n, pub, n_pub, opts, proof, proof_len, transcript);
+  });
+}
+
+int zkp_device_alloc(zkp_ctx* ctx, uint64_t bytes, void** d_ptr) {
+  return guarded(ctx, [&] {
+    if (!d_ptr) return (int)ZKP_ERR_ARGUMENT;
+    HIP_CHECK(hipSetDevice(ctx->device));
+    HIP_CHECK(hipMalloc(d_ptr, bytes ? bytes : 16));
+    ctx->user_allocs.push_back(*d_ptr);
+    return 0;
+  });
+}
+
+int zkp_device_free(zkp_ctx* ctx, void* d_ptr) {
+  return guarded(ctx, [&] {
+    auto it = std::find(ctx->user_allocs.begin(), ctx->user_allocs.end(), d_ptr);
+    if (it == ctx->user_allocs.end()) return (int)ZKP_ERR_ARGUMENT;
+    ctx->user_allocs.erase(it);
+    HIP_CHECK(hipFree(d_ptr));
+    return 0;
+  });
+}
+
+int zkp_copy_to_device(zkp_ctx* ctx, void* d_dst, const void* h_src, uint64_t bytes) {
+  return guarded(ctx, [&] {
+    HIP_CHECK(hipMemcpyAsync(d_dst, h_src, bytes, hipMemcpyHostToDevice, ctx->stream));
+    ctx->sync();
+    return 0;
+  });
+}
+
+int zkp_copy_to_host(zkp_ctx* ctx, void* h_dst, const void* d_src, uint64_t bytes) {
+  return guarded(ctx, [&] {
+    ctx->download(h_dst, d_src, bytes);
+    return 0;
+  });
+}
+
+int zkp_trace_lde_commit(zkp_ctx* ctx, const zkp_felt* trace, uint32_t w, uint64_t n, uint32_t blowup,
+                         zkp_felt* lde_out, uint8_t root[32]) {
+  return guarded(ctx, [&] {
+    HIP_CHECK(hipSetDevice(ctx->device));
+    if (!trace || !root) return (int)ZKP_ERR_ARGUMENT;
+    if (n < 8 || (n & (n - 1)) || w == 0 || w > 255) return (int)ZKP_ERR_TRACE_SHAPE;
+    if (blowup < 2 || (blowup & (blowup - 1)) || blowup > 128) return (int)ZKP_ERR_INVALID_OPTIONS;
+    uint32_t logn = ilog2(n), logB = ilog2(blowup);
+    uint64_t N = n * blowup;
+    felt* d = ctx->buf<felt>("trace_in", (size_t)w * n);
+    ctx->upload(d, trace, (size_t)w * n * 16);
+    felt* coef = ctx->buf<felt>("coef", (size_t)w * n);
+    felt* lde = ctx->buf<felt>("tlde", (size_t)w * N);
+    uint32_t* tree = ctx->buf<uint32_t>("ttree", (size_t)16 * N);
+    lde_commit(ctx, d, w, logn, logB, coef, lde, tree, false, root);
+    if (lde_out) {
+      std::vector<felt> h((size_t)w * N);
+      ctx->download(h.data(), lde, h.size() * 16);
+      for (uint32_t c = 0; c < w; c++)
+        for (uint64_t i = 0; i < N; i++) {
+          felt v = h[((size_t)c * blowup + (i & (blowup - 1))) * n + (i >> logB)];
+          lde_out[(size_t)c * N + i].lo = v.lo;
+          lde_out[(size_t)c * N + i].hi = v.hi;
+        }
+    }
+    ctx->collect_prof();
+    return 0;
+  });
+}
+
+int zkp_merkle_commit_rows(zkp_ctx* ctx, const zkp_felt* cols, uint32_t w, uint64_t rows, uint8_t root[32]) {
+  return guarded(ctx, [&] {
+    HIP_CHECK(hipSetDevice(ctx->device));
+    if (!cols || !root) return (int)ZKP_ERR_ARGUMENT;
+    if (rows < 2 || (rows & (rows - 1)) || w == 0 || w > 255) return (int)ZKP_ERR_TRACE_SHAPE;
+    felt* d = ctx->buf<felt>("mrows", (size_t)w * rows);
+    ctx->upload(d, cols, (size_t)w * rows * 16);
+    uint32_t* tree = ctx->buf<uint32_t>("mtree", (size_t)16 * rows);
+    launch_leaf_hash_lde(ctx->prof, ctx->stream, d, w, 0, rows, tree, rows);
+    launch_merkle_tree(ctx->prof, ctx->stream, tree, rows);
+    ctx->download(root, tree + 8, 32);
+    ctx->collect_prof();
+    return 0;
+  });
+}
+
+int zkp_grind(zkp_ctx* ctx, const uint8_t seed[32], uint32_t bits, uint64_t* nonce) {
+  return guarded(ctx, [&] {
+    HIP_CHECK(hipSetDevice(ctx->device));
+    if (!seed || !nonce || bits > 64) return (int)ZKP_ERR_ARGUMENT;
+    uint32_t sw[8];
+    for (int i = 0; i < 8; i++)
+      sw[i] = (uint32_t)seed[4 * i] | ((uint32_t)seed[4 * i + 1] << 8) | ((uint32_t)seed[4 * i + 2] << 16) |
+              ((uint32_t)seed[4 * i + 3] << 24);
+    unsigned long long* dres = ctx->buf<unsigned long long>("grind_res", 1);
+    const uint64_t chunk = 1ull << 22;
+    for (uint64_t base = 1;; base += chunk) {
+      unsigned long long init = ~0ull, res;
+      ctx->upload(dres, &init, 8);
+      launch_grind(ctx->prof, ctx->stream, sw, base, chunk, bits, dres);
+      ctx->download(&res, dres, 8);
+      if (res != ~0ull) { *nonce = res; break; }
+      if (base > (1ull << 40)) return (int)ZKP_ERR_NONCE;
+    }
+    ctx->collect_prof();
+    return 0;
+  });
+}
+
+int zkp_set_profiling(zkp_ctx* ctx, int enabled) {
+  return guarded(ctx, [&] {
+    ctx->prof.enabled = enabled != 0;
+    return 0;
+  });
+}
+
+int zkp_kernel_stats(zkp_ctx* ctx, const char* kernel_name, uint64_t* launches, double* total_ms) {
+  return guarded(ctx, [&] {
+    if (!kernel_name || !launches || !total_ms) return (int)ZKP_ERR_ARGUMENT;
+    auto it = ctx->stats.find(kernel_name);
+    *launches = it == ctx->stats.end() ? 0 : it->second.first;
+    *total_ms = it == ctx->stats.end() ? 0.0 : it->second.second;
+    return 0;
+  });
+}
+
+int zkp_reset_stats(zkp_ctx* ctx) {
+  return guarded(ctx, [&] {
+    ctx->stats.clear();
+    return 0;
+  });
+}
+
+int zkp_kernel_stats_table(zkp_ctx* ctx, char** table) {
+  return guarded(ctx, [&] {
+    if (!table) return (int)ZKP_ERR_ARGUMENT;
+    std::string s;
+    char line[256];
+    for (auto& kv : ctx->stats) {
+      snprintf(line, sizeof line, "%s %llu %.6f\n", kv.first.c_str(), (unsigned long long)kv.second.first,
+               kv.second.second);
+      s += line;
+    }
+    *table = (char*)malloc(s.size() + 1);
+    memcpy(*table, s.c_str(), s.size() + 1);
+    return 0;
+  });
+}
+
+// Host-side MiMC AIR trace builder (trace construction, like TraceTable building
+// in the reference; not part of the proving hot path).
+int zkp_build_mimc_trace(const uint8_t seed[16], uint64_t n, zkp_felt* out) {
+  if (!seed || !out || n == 0) return ZKP_ERR_ARGUMENT;
+  felt v = from_u128_bytes(seed);
+  if (ge_p(v)) v = sub(v, make(P_LO, P_HI));
+  for (uint64_t i = 0; i < n; i++) {
+    out[i].lo = v.lo;
+    out[i].hi = v.hi;
+    felt u = add(v, felt_u64((i % 64 + 1) * 1000000ull));
+    felt u2 = sqr(u), u3 = mul(u2, u), u6 = sqr(u3);
+    v = mul(u6, u);
+  }
+  return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,120 @@
+// zkp_internal.hpp — declarations shared by the kernel TU and the host prover.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <string>
+#include <vector>
+
+#include "felt.hpp"
+
+// ---------------------------------------------------------------- profiling
+// Every launch goes through Prof::begin/end; when enabled each launch is
+// bracketed by HIP events recorded on the stream it runs on.
+struct ProfRec {
+  const char* name;
+  hipEvent_t start, stop;
+};
+struct Prof {
+  bool enabled = false;
+  std::vector<ProfRec> pending;
+  std::vector<hipEvent_t> pool;
+  hipEvent_t get_event();
+  void begin(const char* name, hipStream_t s);
+  void end(hipStream_t s);
+};
+
+// ---------------------------------------------------------------- NTT
+// One LDS pass of K radix-2 stages (see kernels.hip). `dit` = bit-reversed in
+// -> natural out (Cooley-Tukey); otherwise natural in -> bit-reversed out
+// (Gentleman-Sande). Stages [s0, s0+K).
+struct NttPass {
+  uint32_t logn, s0, K, lo, T, Tl;
+};
+std::vector<NttPass> ntt_plan(uint32_t logn, bool dit);
+
+struct NttBatch {
+  const felt* src;     // batch b reads src + (b / src_div) * src_stride
+  felt* dst;           // batch b writes dst + b * dst_stride
+  const felt* scale;   // nullable; multiplies element p of batch b by scale[(b % scale_mod) * n + p] on load
+  uint64_t src_stride, dst_stride;
+  uint32_t src_div, scale_mod, batches;
+};
+
+// Full transform over `batches` arrays of size 2^logn using twiddle table
+// tw[e] = w_{2^logN}^e (e < 2^logN / 2) of the largest domain (logN >= logn).
+void launch_ntt(Prof& prof, hipStream_t s, const NttBatch& b, uint32_t logn, bool dit, const felt* tw,
+                uint32_t logN);
+
+// ---------------------------------------------------------------- tables
+void launch_expand_powers(Prof& prof, hipStream_t s, felt* out, uint64_t count, const felt* lo_tab,
+                          const felt* hi_tab);
+// S[j*n + p] = ninv * (g * w_N^j)^rev(p)   (j < B)
+void launch_build_coset_scale(Prof& prof, hipStream_t s, felt* S, uint32_t logn, uint32_t B,
+                              const felt* tw, uint32_t logN, const felt* glo, const felt* ghi, felt ninv);
+// Gi[p] = g^-rev(p)
+void launch_build_ginv(Prof& prof, hipStream_t s, felt* Gi, uint32_t logn, const felt* gilo, const felt* gihi);
+
+// ---------------------------------------------------------------- hashing
+// leaves L (= n*B) of a coset-major LDE matrix (cols x B x n) -> nodes[L + i] (8 words each)
+void launch_leaf_hash_lde(Prof& prof, hipStream_t s, const felt* lde, uint32_t cols, uint32_t logB,
+                          uint64_t n, uint32_t* nodes, uint64_t L);
+// leaves of FRI layer: row r = [E[r + k*R] for k < F] -> nodes[R + r]
+void launch_leaf_hash_fri(Prof& prof, hipStream_t s, const felt* E, uint64_t R, uint32_t F, uint32_t* nodes);
+// internal nodes nodes[1..L) from leaves nodes[L..2L)
+void launch_merkle_tree(Prof& prof, hipStream_t s, uint32_t* nodes, uint64_t L);
+void launch_grind(Prof& prof, hipStream_t s, const uint32_t* seed_words_dev, uint64_t base, uint64_t count,
+                  uint32_t bits, unsigned long long* result);
+
+// ---------------------------------------------------------------- constraints
+struct EvalCommon {
+  uint32_t logn, logB, logce, logN;
+  felt g, w_last;        // domain offset (3), w_n^(n-1)
+  const felt* tw;        // w_N^e
+  const felt* zinv;      // ce entries: 1/(x^n - 1) on the CE domain (x^n = g^n * w_ce^s)
+};
+// MiMC: x' - (x + K)^7 ; boundary steps 0 and n-1 on column 0
+struct MimcEvalArgs {
+  felt coef_t, b0, b1, v0, v1;
+  const felt* kper;      // 64*ce periodic values on the CE domain
+};
+void launch_eval_mimc(Prof& prof, hipStream_t s, const EvalCommon& c, const MimcEvalArgs& a, const felt* lde,
+                      felt* comp);
+// linear AIR: T = sum_c a_c*next_c + b_c*cur_c ; one boundary group at step `bstep`:
+// B = sum_c beta_c*cur_c - bconst ; divisor (x - w^bstep)
+struct LinearEvalArgs {
+  uint32_t width;
+  const felt* coefs;     // 3*width: a_c, b_c, beta_c
+  felt bconst, w_bstep;
+};
+void launch_eval_linear(Prof& prof, hipStream_t s, const EvalCommon& c, const LinearEvalArgs& a, const felt* lde,
+                        felt* comp);
+
+// composition segment: A_h[p'] = src[p'*ce + rev(h)] * Gi[p'] * scale_h, h < C
+void launch_segment(Prof& prof, hipStream_t s, const felt* difout, uint32_t logn, uint32_t logce, uint32_t C,
+                    const felt* Gi, const felt* scales_dev, felt* out);
+
+// OOD evaluation of bit-reversed arrays (arrays contiguous, stride n) at x0 and x1
+// partial[(a * nblocks + b) * 2 + {0,1}] ; pw0/pw1 = x^(2^l) tables (logn entries, device)
+void launch_eval_bitrev(Prof& prof, hipStream_t s, const felt* arrays, uint32_t narrays, uint32_t logn,
+                        const felt* pw0, const felt* pw1, felt* partial, uint32_t* nblocks_out);
+
+// DEEP composition over the LDE domain (natural order out)
+struct DeepArgs {
+  uint32_t w, C, logB, logn, logN;
+  const felt* tlde;      // w x B x n
+  const felt* clde;      // C x B x n
+  const felt* gamma;     // w + C
+  felt z, zg, kz, kzg, g;
+  const felt* tw;
+};
+void launch_deep(Prof& prof, hipStream_t s, const DeepArgs& a, felt* out);
+
+// FRI fold-by-F (F = 16): out[r] = q_r(alpha), row r = [E[r + k*R]], x_r = off * w_D^r
+void launch_fri_fold(Prof& prof, hipStream_t s, const felt* E, uint64_t R, uint32_t F, felt alpha, felt off_inv,
+                     const felt* itw, uint32_t logN, uint32_t logD, const felt* eps_inv_dev, felt* out);
+
+// gathers for query openings
+void launch_gather_felts(Prof& prof, hipStream_t s, const felt* src, const uint64_t* idx, felt* out, uint64_t count);
+void launch_gather_digests(Prof& prof, hipStream_t s, const uint32_t* nodes, const uint64_t* idx, uint32_t* out,
+                           uint64_t count);
