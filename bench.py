@@ -1,0 +1,180 @@
+#!/usr/bin/env python3
+"""bench.py — STARK proofs/s on MI355X for the MiMC AIR 2^20-step trace.
+
+Metric (BASELINE.json): "STARK proofs/sec + prove-time ms, MiMC AIR 2^20-step
+trace, 1/2/4/8 MI355X". Workload = BASELINE.json configs[1]:
+MiMC AIR, n = 2^20, x0 = 42e6, ProofOptions(40, 8, 21,
+None, 16, 7, Algebraic, Algebraic). A "step" = one full proof (trace already
+resident in HBM -> serialized proof bytes on the host).
+
+Multi-GPU: one process per GPU (torchrun); each rank proves its own
+independent 2^20 trace on its own device ("replicas", weak scaling — no
+data-path collective). value = total proofs of all
+ranks / max-over-ranks wall time.
+
+Also reported: `roofline` for the dominant kernel (algorithmic bytes per launch
+/ HIP-event launch time on the prover's stream, live in the timed region) and
+`cpu_baseline` (the C oracle restating the winterfell CPU path, one full 2^20
+proof on the host cores; rank 0, N=1 only).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--log-n", type=int, default=20)
+    ap.add_argument("--blowup", type=int, default=8)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-verify", action="store_true")
+    ap.add_argument("--stats", action="store_true", help="print the per-kernel table to stderr")
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as tdist
+        torch.cuda.set_device(local_rank)
+        tdist.init_process_group("nccl")
+        dist = tdist
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    def cuda_sync():
+        if dist is not None:
+            import torch
+            torch.cuda.synchronize()
+
+    from zk_stark_project_amd import AIR_MIMC, MimcProver, ProofOptions
+    from zk_stark_project_amd import _native
+
+    n = 1 << args.log_n
+    opts = ProofOptions(40, args.blowup, 21)  # (40, 8, 21, None, 16, 7, Algebraic, Algebraic)
+    ctx = _native.Context(local_rank)
+    prover = MimcProver(opts, ctx)
+    trace = prover.build_trace(42 * 10**6 + rank, n)  # independent trace per rank
+    pub = prover.get_pub_inputs(trace).to_elements()
+    d_trace = ctx.alloc(trace.data.nbytes)
+    ctx.to_device(d_trace, trace.data)
+
+    proof = None
+    for _ in range(args.warmup):
+        proof, tr = ctx.prove_device(AIR_MIMC, d_trace, 1, n, pub, opts)
+
+    verified = None
+    if rank == 0 and not args.no_verify and proof is not None:
+        import oracle_ref  # noqa: E402  (tests/ checker: verifies the GPU proof)
+        verified = oracle_ref.verify(AIR_MIMC, proof, b"".join(v.to_bytes(16, "little") for v in pub), opts) == 0
+
+    ctx.reset_stats()
+    ctx.set_profiling(True)
+    barrier()
+    cuda_sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        proof, tr = ctx.prove_device(AIR_MIMC, d_trace, 1, n, pub, opts)
+    cuda_sync()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    ctx.set_profiling(False)
+    stats = ctx.stats_table()
+
+    if dist is not None:
+        import torch
+        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local_rank}")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    if rank != 0:
+        if dist is not None:
+            dist.destroy_process_group()
+        return
+
+    total_ms = sum(v["ms"] for v in stats.values())
+    dom_name, dom = max(stats.items(), key=lambda kv: kv[1]["ms"])
+    dom_avg_ms = dom["ms"] / dom["launches"]
+    dom_bytes = dom["bytes"] / dom["launches"]
+    achieved = dom_bytes / (dom_avg_ms * 1e-3) / 1e9
+    roofline = {
+        "bound": "hbm",
+        "kernel": dom_name,
+        "achieved": round(achieved, 2),
+        "peak": HBM_PEAK_GBS,
+        "unit": "GB/s",
+        "frac": round(achieved / HBM_PEAK_GBS, 4),
+        "traffic": None,
+        "bytes_per_launch": dom_bytes,
+        "avg_launch_ms": round(dom_avg_ms, 5),
+        "share_of_device_time": round(dom["ms"] / total_ms, 3) if total_ms else None,
+    }
+
+    cpu = None
+    if world == 1 and not args.no_cpu_baseline:
+        import oracle_ref
+        tb = trace.to_bytes()
+        pb = b"".join(v.to_bytes(16, "little") for v in pub)
+        t1 = time.perf_counter()
+        cproof, _ = oracle_ref.prove(AIR_MIMC, tb, 1, n, pb, opts)
+        dt = time.perf_counter() - t1
+        cpu = {
+            "value": round(1.0 / dt, 5),
+            "unit": "proofs/s",
+            "cores": oracle_ref.lib().oracle_num_threads(),
+            "kind": "port",
+            "sample": f"one full MiMC 2^{args.log_n} proof (C oracle restating the winterfell 0.12 CPU path, "
+                      f"OpenMP), {dt * 1e3:.0f} ms; proof bytes identical to GPU: {cproof == proof}",
+        }
+
+    ms = elapsed / args.steps * 1e3
+    out = {
+        "metric": "STARK proofs/sec + prove-time ms, MiMC AIR 2^20-step trace",
+        "value": round(world * args.steps / elapsed, 3),
+        "unit": "proofs/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f128 (u128 mod 2^128-45*2^40+1)",
+        "data": "synthetic (MiMC trace x0=42e6+rank)",
+        "config": {"workload": f"MiMC AIR 2^{args.log_n}-step trace, blowup={args.blowup} (BASELINE configs[1])",
+                   "trace_length": n, "blowup": args.blowup, "num_queries": 40, "grinding": 21,
+                   "fri_folding": 16, "fri_remainder_max_degree": 7, "parallelism": f"replicas{world}"},
+        "roofline": roofline,
+        "cpu_baseline": cpu,
+        "proof_bytes": len(proof),
+        "verified_by_oracle": verified,
+    }
+    print(json.dumps(out))
+    if args.stats:
+        for k, v in sorted(stats.items(), key=lambda kv: -kv[1]["ms"]):
+            print(f"{k:20s} launches={v['launches']:6d} ms={v['ms']:9.3f} "
+                  f"GB/s={v['bytes'] / (v['ms'] * 1e-3) / 1e9 if v['ms'] else 0:9.1f}", file=sys.stderr)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    main()

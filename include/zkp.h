@@ -163,7 +163,7 @@ int zkp_build_mimc_trace(const uint8_t seed[16], uint64_t n, zkp_felt* out);
 int zkp_set_profiling(zkp_ctx* ctx, int enabled);
 int zkp_kernel_stats(zkp_ctx* ctx, const char* kernel_name, uint64_t* launches, double* total_ms);
 int zkp_reset_stats(zkp_ctx* ctx);
-/* Returns a newline-separated "name launches total_ms" table (free with zkp_free). */
+/* Returns a newline-separated "name launches total_ms algorithmic_bytes" table (free with zkp_free). */
 int zkp_kernel_stats_table(zkp_ctx* ctx, char** table);
 
 #ifdef __cplusplus

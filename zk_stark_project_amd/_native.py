@@ -249,6 +249,6 @@ class Context:
         self.lib.zkp_free(ctypes.cast(p, ctypes.c_void_p))
         out = {}
         for line in txt.splitlines():
-            name, cnt, ms = line.split()
-            out[name] = (int(cnt), float(ms))
+            name, cnt, ms, nbytes = line.split()
+            out[name] = {"launches": int(cnt), "ms": float(ms), "bytes": float(nbytes)}
         return out

@@ -458,10 +458,11 @@ hipEvent_t Prof::get_event() {
   (void)hipEventCreate(&e);
   return e;
 }
-void Prof::begin(const char* name, hipStream_t s) {
+void Prof::begin(const char* name, hipStream_t s, double bytes) {
   if (!enabled) return;
   ProfRec r;
   r.name = name;
+  r.bytes = bytes;
   r.start = get_event();
   r.stop = get_event();
   (void)hipEventRecord(r.start, s);
@@ -472,9 +473,9 @@ void Prof::end(hipStream_t s) {
   (void)hipEventRecord(pending.back().stop, s);
 }
 
-#define LAUNCH(prof, name, stream, ...)                        \
+#define LAUNCH(prof, name, stream, bytes, ...)                 \
   do {                                                          \
-    (prof).begin(name, stream);                                 \
+    (prof).begin(name, stream, (double)(bytes));                \
     __VA_ARGS__;                                                \
     (prof).end(stream);                                         \
   } while (0)
@@ -530,7 +531,7 @@ void launch_ntt(Prof& prof, hipStream_t s, const NttBatch& b, uint32_t logn, boo
     uint64_t groups = 1ull << (logn - ps.K);
     dim3 grid((uint32_t)(groups / ps.T), b.batches);
     size_t shmem = (size_t)(ps.T << ps.K) * sizeof(felt);
-    LAUNCH(prof, dit ? "ntt_dit_pass" : "ntt_dif_pass", s,
+    LAUNCH(prof, dit ? "ntt_dit_pass" : "ntt_dif_pass", s, (double)b.batches * (1ull << logn) * 16.0 * (a.scale ? 3 : 2),
            hipLaunchKernelGGL(k_ntt_pass, grid, dim3(TPB), shmem, s, a));
     first = false;
   }
@@ -538,56 +539,56 @@ void launch_ntt(Prof& prof, hipStream_t s, const NttBatch& b, uint32_t logn, boo
 
 void launch_expand_powers(Prof& prof, hipStream_t s, felt* out, uint64_t count, const felt* lo_tab,
                           const felt* hi_tab) {
-  LAUNCH(prof, "expand_powers", s,
+  LAUNCH(prof, "expand_powers", s, count * 16.0,
          hipLaunchKernelGGL(k_expand_powers, dim3(grid_stride_blocks(count)), dim3(TPB), 0, s, out, count, lo_tab,
                             hi_tab));
 }
 
 void launch_build_coset_scale(Prof& prof, hipStream_t s, felt* S, uint32_t logn, uint32_t B, const felt* tw,
                               uint32_t logN, const felt* glo, const felt* ghi, felt ninv) {
-  LAUNCH(prof, "build_coset_scale", s,
+  LAUNCH(prof, "build_coset_scale", s, (double)((uint64_t)B << logn) * 16.0,
          hipLaunchKernelGGL(k_build_coset_scale, dim3(grid_stride_blocks((uint64_t)B << logn)), dim3(TPB), 0, s, S,
                             logn, B, tw, logN, glo, ghi, ninv));
 }
 
 void launch_build_ginv(Prof& prof, hipStream_t s, felt* Gi, uint32_t logn, const felt* gilo, const felt* gihi) {
-  LAUNCH(prof, "build_ginv", s,
+  LAUNCH(prof, "build_ginv", s, (double)(1ull << logn) * 16.0,
          hipLaunchKernelGGL(k_build_ginv, dim3(grid_stride_blocks(1ull << logn)), dim3(TPB), 0, s, Gi, logn, gilo,
                             gihi));
 }
 
 void launch_leaf_hash_lde(Prof& prof, hipStream_t s, const felt* lde, uint32_t cols, uint32_t logB, uint64_t n,
                           uint32_t* nodes, uint64_t L) {
-  LAUNCH(prof, "leaf_hash_lde", s,
+  LAUNCH(prof, "leaf_hash_lde", s, (double)L * (cols * 16.0 + 32.0),
          hipLaunchKernelGGL(k_leaf_hash_lde, dim3(blocks_for(L)), dim3(TPB), 0, s, lde, cols, logB, n, nodes, L));
 }
 
 void launch_leaf_hash_fri(Prof& prof, hipStream_t s, const felt* E, uint64_t R, uint32_t F, uint32_t* nodes) {
-  LAUNCH(prof, "leaf_hash_fri", s,
+  LAUNCH(prof, "leaf_hash_fri", s, (double)R * (F * 16.0 + 32.0),
          hipLaunchKernelGGL(k_leaf_hash_fri, dim3(blocks_for(R)), dim3(TPB), 0, s, E, R, F, nodes));
 }
 
 void launch_merkle_tree(Prof& prof, hipStream_t s, uint32_t* nodes, uint64_t L) {
   uint64_t lvl = L / 2;
   for (; lvl >= 2048; lvl >>= 1)
-    LAUNCH(prof, "merkle_level", s,
+    LAUNCH(prof, "merkle_level", s, (double)lvl * 96.0,
            hipLaunchKernelGGL(k_merkle_level, dim3(blocks_for(lvl)), dim3(TPB), 0, s, nodes, lvl));
   if (lvl >= 1)
-    LAUNCH(prof, "merkle_top", s, hipLaunchKernelGGL(k_merkle_top, dim3(1), dim3(1024), 0, s, nodes, lvl));
+    LAUNCH(prof, "merkle_top", s, (double)lvl * 2.0 * 96.0, hipLaunchKernelGGL(k_merkle_top, dim3(1), dim3(1024), 0, s, nodes, lvl));
 }
 
 void launch_grind(Prof& prof, hipStream_t s, const uint32_t* seed_words, uint64_t base, uint64_t count,
                   uint32_t bits, unsigned long long* result) {
   SeedArg sa;
   for (int i = 0; i < 8; i++) sa.w[i] = seed_words[i];
-  LAUNCH(prof, "grind", s,
+  LAUNCH(prof, "grind", s, 0.0,
          hipLaunchKernelGGL(k_grind, dim3(blocks_for(count)), dim3(TPB), 0, s, sa, base, count, bits, result));
 }
 
 void launch_eval_mimc(Prof& prof, hipStream_t s, const EvalCommon& c, const MimcEvalArgs& a, const felt* lde,
                       felt* comp) {
   uint64_t M = 1ull << (c.logn + c.logce);
-  LAUNCH(prof, "eval_mimc", s,
+  LAUNCH(prof, "eval_mimc", s, (double)M * 32.0,
          hipLaunchKernelGGL(k_eval_mimc, dim3(blocks_for((M + EVAL_CH - 1) / EVAL_CH)), dim3(TPB), 0, s, c, a, lde,
                             comp));
 }
@@ -595,14 +596,14 @@ void launch_eval_mimc(Prof& prof, hipStream_t s, const EvalCommon& c, const Mimc
 void launch_eval_linear(Prof& prof, hipStream_t s, const EvalCommon& c, const LinearEvalArgs& a, const felt* lde,
                         felt* comp) {
   uint64_t M = 1ull << (c.logn + c.logce);
-  LAUNCH(prof, "eval_linear", s,
+  LAUNCH(prof, "eval_linear", s, (double)M * (a.width * 16.0 + 16.0),
          hipLaunchKernelGGL(k_eval_linear, dim3(blocks_for((M + EVAL_CH - 1) / EVAL_CH)), dim3(TPB), 0, s, c, a, lde,
                             comp));
 }
 
 void launch_segment(Prof& prof, hipStream_t s, const felt* difout, uint32_t logn, uint32_t logce, uint32_t C,
                     const felt* Gi, const felt* scales, felt* out) {
-  LAUNCH(prof, "segment", s,
+  LAUNCH(prof, "segment", s, (double)((uint64_t)C << logn) * 48.0,
          hipLaunchKernelGGL(k_segment, dim3(grid_stride_blocks((uint64_t)C << logn)), dim3(TPB), 0, s, difout, logn,
                             logce, C, Gi, scales, out));
 }
@@ -612,14 +613,14 @@ void launch_eval_bitrev(Prof& prof, hipStream_t s, const felt* arrays, uint32_t 
   uint32_t logE = logn < OOD_LOGE ? logn : OOD_LOGE;
   uint32_t nb = 1u << (logn - logE);
   *nblocks_out = nb;
-  LAUNCH(prof, "eval_bitrev", s,
+  LAUNCH(prof, "eval_bitrev", s, (double)narrays * (1ull << logn) * 16.0,
          hipLaunchKernelGGL(k_eval_bitrev, dim3(nb, narrays), dim3(TPB), 0, s, arrays, logn, logE, pw0, pw1,
                             partial));
 }
 
 void launch_deep(Prof& prof, hipStream_t s, const DeepArgs& a, felt* out) {
   uint64_t N = 1ull << a.logN;
-  LAUNCH(prof, "deep", s,
+  LAUNCH(prof, "deep", s, (double)N * ((a.w + a.C) * 16.0 + 16.0),
          hipLaunchKernelGGL(k_deep, dim3(blocks_for((N + EVAL_CH - 1) / EVAL_CH)), dim3(TPB), 0, s, a, out));
 }
 
@@ -627,18 +628,18 @@ void launch_fri_fold(Prof& prof, hipStream_t s, const felt* E, uint64_t R, uint3
                      const felt* itw, uint32_t logN, uint32_t logD, const felt* eps_inv, felt* out) {
   (void)F;  // only 16 is compiled (the reference's fri_folding_factor)
   uint32_t xsh = logN - logD;
-  LAUNCH(prof, "fri_fold16", s,
+  LAUNCH(prof, "fri_fold16", s, (double)R * (16 * 16.0 + 16.0),
          hipLaunchKernelGGL(k_fri_fold16, dim3(blocks_for(R)), dim3(TPB), 0, s, E, R, alpha, off_inv, itw, xsh,
                             eps_inv, out));
 }
 
 void launch_gather_felts(Prof& prof, hipStream_t s, const felt* src, const uint64_t* idx, felt* out, uint64_t count) {
-  LAUNCH(prof, "gather", s,
+  LAUNCH(prof, "gather", s, count * 32.0,
          hipLaunchKernelGGL(k_gather_felts, dim3(blocks_for(count)), dim3(TPB), 0, s, src, idx, out, count));
 }
 
 void launch_gather_digests(Prof& prof, hipStream_t s, const uint32_t* nodes, const uint64_t* idx, uint32_t* out,
                            uint64_t count) {
-  LAUNCH(prof, "gather", s,
+  LAUNCH(prof, "gather", s, count * 40.0,
          hipLaunchKernelGGL(k_gather_digests, dim3(blocks_for(count)), dim3(TPB), 0, s, nodes, idx, out, count));
 }

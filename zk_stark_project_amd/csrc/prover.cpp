@@ -336,7 +336,11 @@ struct zkp_ctx {
   Prof prof;
   std::string err;
   std::map<std::string, DevBuf> bufs;
-  std::map<std::string, std::pair<uint64_t, double>> stats;
+  struct Stat {
+    uint64_t launches = 0;
+    double ms = 0, bytes = 0;
+  };
+  std::map<std::string, Stat> stats;
   std::vector<void*> user_allocs;
 
   template <typename T>
@@ -367,8 +371,9 @@ struct zkp_ctx {
       float ms = 0;
       HIP_CHECK(hipEventElapsedTime(&ms, r.start, r.stop));
       auto& s = stats[r.name];
-      s.first += 1;
-      s.second += ms;
+      s.launches += 1;
+      s.ms += ms;
+      s.bytes += r.bytes;
       prof.pool.push_back(r.start);
       prof.pool.push_back(r.stop);
     }
@@ -1044,8 +1049,8 @@ int zkp_kernel_stats(zkp_ctx* ctx, const char* kernel_name, uint64_t* launches, 
   return guarded(ctx, [&] {
     if (!kernel_name || !launches || !total_ms) return (int)ZKP_ERR_ARGUMENT;
     auto it = ctx->stats.find(kernel_name);
-    *launches = it == ctx->stats.end() ? 0 : it->second.first;
-    *total_ms = it == ctx->stats.end() ? 0.0 : it->second.second;
+    *launches = it == ctx->stats.end() ? 0 : it->second.launches;
+    *total_ms = it == ctx->stats.end() ? 0.0 : it->second.ms;
     return 0;
   });
 }
@@ -1063,8 +1068,8 @@ int zkp_kernel_stats_table(zkp_ctx* ctx, char** table) {
     std::string s;
     char line[256];
     for (auto& kv : ctx->stats) {
-      snprintf(line, sizeof line, "%s %llu %.6f\n", kv.first.c_str(), (unsigned long long)kv.second.first,
-               kv.second.second);
+      snprintf(line, sizeof line, "%s %llu %.6f %.0f\n", kv.first.c_str(), (unsigned long long)kv.second.launches,
+               kv.second.ms, kv.second.bytes);
       s += line;
     }
     *table = (char*)malloc(s.size() + 1);

@@ -13,6 +13,7 @@
 // bracketed by HIP events recorded on the stream it runs on.
 struct ProfRec {
   const char* name;
+  double bytes;  // algorithmic (compulsory) HBM bytes of this launch
   hipEvent_t start, stop;
 };
 struct Prof {
@@ -20,7 +21,7 @@ struct Prof {
   std::vector<ProfRec> pending;
   std::vector<hipEvent_t> pool;
   hipEvent_t get_event();
-  void begin(const char* name, hipStream_t s);
+  void begin(const char* name, hipStream_t s, double bytes);
   void end(hipStream_t s);
 };
 
