@@ -55,10 +55,6 @@ def main():
         tdist.init_process_group("nccl")
         dist = tdist
 
-    def barrier():
-        if dist is not None:
-            dist.barrier()
-
     def cuda_sync():
         if dist is not None:
             import torch
@@ -76,33 +72,26 @@ def main():
     d_trace = ctx.alloc(trace.data.nbytes)
     ctx.to_device(d_trace, trace.data)
 
-    proof = None
-    for _ in range(args.warmup):
-        proof, tr = ctx.prove_device(AIR_MIMC, d_trace, 1, n, pub, opts)
+    from zk_stark_project_amd.replicas import aggregate_rate, timed_replicas
+
+    def prove_once():
+        return ctx.prove_device(AIR_MIMC, d_trace, 1, n, pub, opts)
 
     verified = None
-    if rank == 0 and not args.no_verify and proof is not None:
-        import oracle_ref  # noqa: E402  (tests/ checker: verifies the GPU proof)
-        verified = oracle_ref.verify(AIR_MIMC, proof, b"".join(v.to_bytes(16, "little") for v in pub), opts) == 0
+    if args.warmup > 0:
+        proof, _ = prove_once()
+        if rank == 0 and not args.no_verify:
+            import oracle_ref  # tests/ checker: the oracle's verifier accepts the GPU proof
+            verified = oracle_ref.verify(AIR_MIMC, proof, b"".join(v.to_bytes(16, "little") for v in pub),
+                                         opts) == 0
 
     ctx.reset_stats()
     ctx.set_profiling(True)
-    barrier()
-    cuda_sync()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        proof, tr = ctx.prove_device(AIR_MIMC, d_trace, 1, n, pub, opts)
-    cuda_sync()
-    barrier()
-    elapsed = time.perf_counter() - t0
+    elapsed, _, (proof, tr) = timed_replicas(prove_once, args.steps, max(args.warmup - 1, 0), dist=dist,
+                                              device_sync=cuda_sync if dist is not None else None,
+                                              device=f"cuda:{local_rank}")
     ctx.set_profiling(False)
     stats = ctx.stats_table()
-
-    if dist is not None:
-        import torch
-        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local_rank}")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
 
     if rank != 0:
         if dist is not None:
@@ -147,7 +136,7 @@ def main():
     ms = elapsed / args.steps * 1e3
     out = {
         "metric": "STARK proofs/sec + prove-time ms, MiMC AIR 2^20-step trace",
-        "value": round(world * args.steps / elapsed, 3),
+        "value": round(aggregate_rate(world, args.steps, elapsed), 3),
         "unit": "proofs/s",
         "n_gpus": world,
         "steps": args.steps,
