@@ -21,7 +21,9 @@ def rand_trace(w, n, seed):
     return a
 
 
-@pytest.mark.parametrize("w,n,blowup", [(1, 8, 2), (1, 64, 8), (3, 256, 4), (120, 16, 16), (2, 1024, 8)])
+@pytest.mark.parametrize("w,n,blowup", [(1, 8, 2), (1, 64, 8), (3, 256, 4), (120, 16, 16), (2, 1024, 8),
+                                         (1, 4096, 8), (2, 8192, 4), (1, 1 << 15, 2), (3, 1 << 13, 16),
+                                         (1, 1 << 17, 8)])
 def test_trace_lde_commit_matches_oracle(ctx, w, n, blowup):
     tr = rand_trace(w, n, seed=w * 1000 + n)
     lde, root = ctx.trace_lde_commit(tr, blowup)
@@ -51,7 +53,8 @@ def mimc_case(n, opts):
 
 
 @pytest.mark.parametrize("n,blowup,q,grind", [(64, 8, 40, 8), (128, 8, 40, 0), (256, 16, 24, 4),
-                                              (1024, 8, 40, 16), (4096, 8, 40, 12)])
+                                              (1024, 8, 40, 16), (4096, 8, 40, 12), (1 << 14, 8, 40, 21),
+                                              (1 << 16, 8, 40, 21), (1 << 13, 32, 30, 10)])
 def test_mimc_proof_bit_exact(ctx, n, blowup, q, grind):
     opts = ProofOptions(q, blowup, grind)
     p, trace = mimc_case(n, opts)
@@ -76,7 +79,7 @@ def gu_prover(ndev, n, opts, seed):
                               blinding=[r() for _ in range(60)])
 
 
-@pytest.mark.parametrize("ndev,n", [(2, 8), (6, 64), (30, 256)])
+@pytest.mark.parametrize("ndev,n", [(2, 8), (6, 64), (30, 256), (64, 1 << 12)])
 def test_global_update_proof_bit_exact(ctx, ndev, n):
     opts = ProofOptions(40, 16, 8)
     p = gu_prover(ndev, n, opts, seed=ndev)

@@ -32,7 +32,7 @@ ZKP_HD felt from_u64(uint64_t v) { return make(v, 0); }
 ZKP_HD bool eq(felt a, felt b) { return a.lo == b.lo && a.hi == b.hi; }
 ZKP_HD bool is_zero(felt a) { return (a.lo | a.hi) == 0; }
 
-ZKP_HD felt add(felt a, felt b) {
+ZKP_HD felt add_portable(felt a, felt b) {
   unsigned long long c1, c2, c3, c4;
   uint64_t s0 = __builtin_addcll(a.lo, b.lo, 0ULL, &c1);
   uint64_t s1 = __builtin_addcll(a.hi, b.hi, c1, &c2);
@@ -43,7 +43,7 @@ ZKP_HD felt add(felt a, felt b) {
   return make(take ? t0 : s0, take ? t1 : s1);
 }
 
-ZKP_HD felt sub(felt a, felt b) {
+ZKP_HD felt sub_portable(felt a, felt b) {
   unsigned long long b1, b2, c1, c2;
   uint64_t d0 = __builtin_subcll(a.lo, b.lo, 0ULL, &b1);
   uint64_t d1 = __builtin_subcll(a.hi, b.hi, b1, &b2);
@@ -53,7 +53,6 @@ ZKP_HD felt sub(felt a, felt b) {
   return make(b2 ? e0 : d0, b2 ? e1 : d1);
 }
 
-ZKP_HD felt neg(felt a) { return sub(zero(), a); }
 
 // reduce the 256-bit product r[0..7] (32-bit limbs, little-endian)
 ZKP_HD felt reduce8(const uint32_t r[8]) {
@@ -111,7 +110,7 @@ ZKP_HD felt reduce8(const uint32_t r[8]) {
   return c4 ? make(t0, t1) : make(lo, hi);
 }
 
-ZKP_HD felt mul(felt a, felt b) {
+ZKP_HD felt mul_portable(felt a, felt b) {
   const uint32_t x0 = (uint32_t)a.lo, x1 = (uint32_t)(a.lo >> 32), x2 = (uint32_t)a.hi, x3 = (uint32_t)(a.hi >> 32);
   const uint32_t y0 = (uint32_t)b.lo, y1 = (uint32_t)(b.lo >> 32), y2 = (uint32_t)b.hi, y3 = (uint32_t)(b.hi >> 32);
   uint32_t r[8];
@@ -135,6 +134,37 @@ ZKP_HD felt mul(felt a, felt b) {
   return reduce8(r);
 }
 
+}  // namespace fp
+
+#if defined(__HIP_DEVICE_COMPILE__)
+#include "felt_dev.hpp"
+#endif
+
+namespace fp {
+
+// Public field ops: carry-chain asm on gfx950 (felt_dev.hpp), portable C on the host.
+ZKP_HD felt add(felt a, felt b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return fpd::add(a, b);
+#else
+  return add_portable(a, b);
+#endif
+}
+ZKP_HD felt sub(felt a, felt b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return fpd::sub(a, b);
+#else
+  return sub_portable(a, b);
+#endif
+}
+ZKP_HD felt mul(felt a, felt b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return fpd::mul(a, b);
+#else
+  return mul_portable(a, b);
+#endif
+}
+ZKP_HD felt neg(felt a) { return sub(zero(), a); }
 ZKP_HD felt sqr(felt a) { return mul(a, a); }
 
 ZKP_HD felt pow_u64(felt b, uint64_t e) {

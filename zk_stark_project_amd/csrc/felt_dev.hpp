@@ -1,0 +1,219 @@
+// felt_dev.hpp — gfx950 carry-chain implementations of the f128 field ops.
+//
+// hipcc lowers 64-bit add-with-carry to 64-bit adds + 64-bit compares +
+// selects; here every carry lives in an SGPR pair (the per-lane carry mask)
+// and flows through v_add_co/v_addc_co/v_sub_co/v_subb_co and the carry-out of
+// v_mad_u64_u32, so a 128-bit add is 4 VALU ops + the select. Only the
+// instruction choice is pinned (non-volatile asm): scheduling and register
+// allocation stay with the compiler. Semantics are identical to the portable
+// versions in felt.hpp (checked bit-exactly by the GPU parity tests).
+#pragma once
+#include <stdint.h>
+// included from felt.hpp inside the device compilation pass only
+
+namespace fpd {
+
+// ---- 32-bit carry-chain primitives (carry masks in SGPR pairs)
+__device__ __forceinline__ uint32_t add_co(uint32_t a, uint32_t b, uint64_t& co) {
+  uint32_t r;
+  asm("v_add_co_u32_e64 %0, %1, %2, %3" : "=v"(r), "=s"(co) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ uint32_t addc_co(uint32_t a, uint32_t b, uint64_t ci, uint64_t& co) {
+  uint32_t r;
+  asm("v_addc_co_u32_e64 %0, %1, %2, %3, %4" : "=v"(r), "=s"(co) : "v"(a), "v"(b), "s"(ci));
+  return r;
+}
+__device__ __forceinline__ uint32_t addc(uint32_t a, uint32_t b, uint64_t ci) {
+  uint32_t r;
+  uint64_t dead;
+  asm("v_addc_co_u32_e64 %0, %1, %2, %3, %4" : "=v"(r), "=s"(dead) : "v"(a), "v"(b), "s"(ci));
+  return r;
+}
+__device__ __forceinline__ uint32_t sub_co(uint32_t a, uint32_t b, uint64_t& bo) {
+  uint32_t r;
+  asm("v_sub_co_u32_e64 %0, %1, %2, %3" : "=v"(r), "=s"(bo) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ uint32_t subb_co(uint32_t a, uint32_t b, uint64_t bi, uint64_t& bo) {
+  uint32_t r;
+  asm("v_subb_co_u32_e64 %0, %1, %2, %3, %4" : "=v"(r), "=s"(bo) : "v"(a), "v"(b), "s"(bi));
+  return r;
+}
+__device__ __forceinline__ uint32_t subb(uint32_t a, uint32_t b, uint64_t bi) {
+  uint32_t r;
+  uint64_t dead;
+  asm("v_subb_co_u32_e64 %0, %1, %2, %3, %4" : "=v"(r), "=s"(dead) : "v"(a), "v"(b), "s"(bi));
+  return r;
+}
+// d = a*b + c (64-bit), carry-out of the 64-bit add in co
+__device__ __forceinline__ uint64_t mad_co(uint32_t a, uint32_t b, uint64_t c, uint64_t& co) {
+  uint64_t d;
+  asm("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=v"(d), "=s"(co) : "v"(a), "v"(b), "v"(c));
+  return d;
+}
+__device__ __forceinline__ uint64_t mad(uint32_t a, uint32_t b, uint64_t c) {
+  uint64_t d, dead;
+  asm("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=v"(d), "=s"(dead) : "v"(a), "v"(b), "v"(c));
+  return d;
+}
+__device__ __forceinline__ uint64_t or_mask(uint64_t a, uint64_t b) {
+  uint64_t r;
+  asm("s_or_b64 %0, %1, %2" : "=s"(r) : "s"(a), "s"(b) : "scc");
+  return r;
+}
+__device__ __forceinline__ uint32_t sel(uint32_t f, uint32_t t, uint64_t m) {  // m ? t : f
+  uint32_t r;
+  asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(f), "v"(t), "s"(m));
+  return r;
+}
+
+struct L4 {
+  uint32_t w0, w1, w2, w3;
+};
+__device__ __forceinline__ L4 split(felt a) {
+  return {(uint32_t)a.lo, (uint32_t)(a.lo >> 32), (uint32_t)a.hi, (uint32_t)(a.hi >> 32)};
+}
+__device__ __forceinline__ felt join(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3) {
+  felt r;
+  r.lo = (uint64_t)w0 | ((uint64_t)w1 << 32);
+  r.hi = (uint64_t)w2 | ((uint64_t)w3 << 32);
+  return r;
+}
+
+constexpr uint32_t C0 = 0xffffffffu;  // 2^128 - p = 0x2cff_ffffffff
+constexpr uint32_t C1 = 0x2cffu;
+constexpr uint32_t P1 = 0xffffd300u;  // p = 0xffffffff_ffffffff_ffffd300_00000001
+
+// s + C (= s - p mod 2^128) with its carry-out; result = (k | carry) ? s - p : s
+__device__ __forceinline__ felt canon_from(uint32_t s0, uint32_t s1, uint32_t s2, uint32_t s3, uint64_t k) {
+  uint64_t c;
+  uint32_t t0 = add_co(s0, C0, c);
+  uint32_t t1 = addc_co(s1, C1, c, c);
+  uint32_t t2 = addc_co(s2, 0u, c, c);
+  uint32_t t3 = addc_co(s3, 0u, c, c);
+  uint64_t m = or_mask(k, c);
+  return join(sel(s0, t0, m), sel(s1, t1, m), sel(s2, t2, m), sel(s3, t3, m));
+}
+
+__device__ __forceinline__ felt add(felt a, felt b) {
+  L4 x = split(a), y = split(b);
+  uint64_t c;
+  uint32_t s0 = add_co(x.w0, y.w0, c);
+  uint32_t s1 = addc_co(x.w1, y.w1, c, c);
+  uint32_t s2 = addc_co(x.w2, y.w2, c, c);
+  uint32_t s3 = addc_co(x.w3, y.w3, c, c);
+  return canon_from(s0, s1, s2, s3, c);
+}
+
+__device__ __forceinline__ felt sub(felt a, felt b) {
+  L4 x = split(a), y = split(b);
+  uint64_t bw;
+  uint32_t d0 = sub_co(x.w0, y.w0, bw);
+  uint32_t d1 = subb_co(x.w1, y.w1, bw, bw);
+  uint32_t d2 = subb_co(x.w2, y.w2, bw, bw);
+  uint32_t d3 = subb_co(x.w3, y.w3, bw, bw);
+  // on borrow: d - C (mod 2^128) == d + p
+  uint32_t m0 = sel(0u, C0, bw), m1 = sel(0u, C1, bw);
+  uint64_t b2;
+  uint32_t e0 = sub_co(d0, m0, b2);
+  uint32_t e1 = subb_co(d1, m1, b2, b2);
+  uint32_t e2 = subb_co(d2, 0u, b2, b2);
+  uint32_t e3 = subb(d3, 0u, b2);
+  return join(e0, e1, e2, e3);
+}
+
+// 256-bit product in 32-bit limbs (product scanning, 96-bit column accumulator)
+__device__ __forceinline__ void mul256(L4 x, L4 y, uint32_t r[8]) {
+  uint64_t acc, c;
+  uint32_t ov;
+  // column 0
+  acc = mad(x.w0, y.w0, 0ull);
+  r[0] = (uint32_t)acc;
+  acc >>= 32;
+  // column 1
+  acc = mad_co(x.w0, y.w1, acc, c); ov = addc(0u, 0u, c);
+  acc = mad_co(x.w1, y.w0, acc, c); ov = addc(ov, 0u, c);
+  r[1] = (uint32_t)acc;
+  acc = (acc >> 32) | ((uint64_t)ov << 32);
+  // column 2
+  acc = mad_co(x.w0, y.w2, acc, c); ov = addc(0u, 0u, c);
+  acc = mad_co(x.w1, y.w1, acc, c); ov = addc(ov, 0u, c);
+  acc = mad_co(x.w2, y.w0, acc, c); ov = addc(ov, 0u, c);
+  r[2] = (uint32_t)acc;
+  acc = (acc >> 32) | ((uint64_t)ov << 32);
+  // column 3
+  acc = mad_co(x.w0, y.w3, acc, c); ov = addc(0u, 0u, c);
+  acc = mad_co(x.w1, y.w2, acc, c); ov = addc(ov, 0u, c);
+  acc = mad_co(x.w2, y.w1, acc, c); ov = addc(ov, 0u, c);
+  acc = mad_co(x.w3, y.w0, acc, c); ov = addc(ov, 0u, c);
+  r[3] = (uint32_t)acc;
+  acc = (acc >> 32) | ((uint64_t)ov << 32);
+  // column 4
+  acc = mad_co(x.w1, y.w3, acc, c); ov = addc(0u, 0u, c);
+  acc = mad_co(x.w2, y.w2, acc, c); ov = addc(ov, 0u, c);
+  acc = mad_co(x.w3, y.w1, acc, c); ov = addc(ov, 0u, c);
+  r[4] = (uint32_t)acc;
+  acc = (acc >> 32) | ((uint64_t)ov << 32);
+  // column 5
+  acc = mad_co(x.w2, y.w3, acc, c); ov = addc(0u, 0u, c);
+  acc = mad_co(x.w3, y.w2, acc, c); ov = addc(ov, 0u, c);
+  r[5] = (uint32_t)acc;
+  acc = (acc >> 32) | ((uint64_t)ov << 32);
+  // column 6 (cannot overflow: the full product is < 2^256)
+  acc = mad(x.w3, y.w3, acc);
+  r[6] = (uint32_t)acc;
+  r[7] = (uint32_t)(acc >> 32);
+}
+
+// reduce hi*2^128 + lo with 2^128 = 0x2D00*2^32 - 1 (mod p)
+__device__ __forceinline__ felt reduce(const uint32_t r[8]) {
+  const uint32_t K = 0x2d00u;  // 45 * 2^8
+  // q = H * K (5 limbs)
+  uint64_t t = mad(r[4], K, 0ull);
+  uint32_t q0 = (uint32_t)t;
+  t = mad(r[5], K, t >> 32);
+  uint32_t q1 = (uint32_t)t;
+  t = mad(r[6], K, t >> 32);
+  uint32_t q2 = (uint32_t)t;
+  t = mad(r[7], K, t >> 32);
+  uint32_t q3 = (uint32_t)t, q4 = (uint32_t)(t >> 32);
+  // X = L + q*2^32 - H  (6 limbs, X >= 0, X < 2^175)
+  uint64_t c;
+  uint32_t s1 = add_co(r[1], q0, c);
+  uint32_t s2 = addc_co(r[2], q1, c, c);
+  uint32_t s3 = addc_co(r[3], q2, c, c);
+  uint32_t s4 = addc_co(q3, 0u, c, c);
+  uint32_t s5 = addc(q4, 0u, c);
+  uint64_t b;
+  uint32_t x0 = sub_co(r[0], r[4], b);
+  uint32_t x1 = subb_co(s1, r[5], b, b);
+  uint32_t x2 = subb_co(s2, r[6], b, b);
+  uint32_t x3 = subb_co(s3, r[7], b, b);
+  uint32_t x4 = subb_co(s4, 0u, b, b);
+  uint32_t x5 = subb(s5, 0u, b);
+  // Y = Xl + (Xh*K)*2^32 - Xh, Xh = x4 + x5*2^32 < 2^47
+  uint64_t u = mad(x4, K, 0ull);
+  uint32_t u0 = (uint32_t)u;
+  uint32_t u1 = (uint32_t)(u >> 32) + x5 * K;  // < 2^29
+  uint32_t y1 = add_co(x1, u0, c);
+  uint32_t y2 = addc_co(x2, u1, c, c);
+  uint32_t y3 = addc_co(x3, 0u, c, c);
+  uint64_t top = c;  // carry past 2^128
+  uint32_t z0 = sub_co(x0, x4, b);
+  uint32_t z1 = subb_co(y1, x5, b, b);
+  uint32_t z2 = subb_co(y2, 0u, b, b);
+  uint32_t z3 = subb_co(y3, 0u, b, b);
+  // net bit 128 = top - borrow (>= 0 overall); set when top & !borrow
+  uint64_t k;
+  asm("s_andn2_b64 %0, %1, %2" : "=s"(k) : "s"(top), "s"(b) : "scc");
+  return canon_from(z0, z1, z2, z3, k);
+}
+
+__device__ __forceinline__ felt mul(felt a, felt b) {
+  uint32_t r[8];
+  mul256(split(a), split(b), r);
+  return reduce(r);
+}
+
+}  // namespace fpd

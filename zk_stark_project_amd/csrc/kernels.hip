@@ -11,6 +11,8 @@
 #include "zkp_internal.hpp"
 #include "blake3.hpp"
 
+#include <type_traits>
+
 using namespace fp;
 
 #define TPB 256
@@ -19,6 +21,15 @@ namespace {
 
 __device__ __forceinline__ uint32_t rev_bits(uint32_t x, uint32_t bits) {
   return bits == 0 ? 0u : (__brev(x) >> (32 - bits));
+}
+
+// compile-time unrolled loop: f(std::integral_constant<int, I>) for I in [B, E)
+template <int B, int E, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (B < E) {
+    f(std::integral_constant<int, B>{});
+    static_for<B + 1, E>(f);
+  }
 }
 
 // w_N^e for e < N (table holds e < N/2; w_N^(N/2) = -1)
@@ -111,6 +122,154 @@ __global__ __launch_bounds__(TPB) void k_ntt_pass(NttKArgs a) {
     uint64_t addr = ((hi0 + hl) << (lo + K)) + ((uint64_t)q << lo) + l0 + ll;
     dst[addr] = lds[(q << a.logT) + (hl * Tl) + ll];
   }
+}
+
+// ------------------------------------------------------------- NTT radix-8
+// Register-blocked pass: each of NT threads owns 8 elements; a pass of K <= 10
+// stages runs as rounds of up to 3 stages (radix-8 / 2x radix-4 / 4x radix-2)
+// in registers with one LDS exchange per round. Global traffic is staged
+// through LDS in the coalesced (gg-fastest) order.
+struct Ntt8Args {
+  const felt* src;
+  felt* dst;
+  const felt* scale;
+  const felt* tw;
+  uint64_t src_stride, dst_stride;
+  uint32_t src_div, scale_mod;
+  uint32_t logn, s0, K, lo, logT, logTl, tw_shift, nrounds;
+  uint32_t rbits[4];
+};
+
+template <bool DIT>
+__device__ __forceinline__ felt ntt_tw(const Ntt8Args& a, uint64_t j, uint32_t pbit) {
+  uint32_t s = DIT ? a.s0 + pbit : a.s0 + a.K - 1 - pbit;
+  uint32_t sh = DIT ? (a.logn - 1 - s + a.tw_shift) : (s + a.tw_shift);
+  return a.tw[j << sh];
+}
+
+template <bool DIT>
+__device__ __forceinline__ void bfly(felt& x, felt& y, felt w) {
+  if (DIT) {
+    felt t = mul(y, w);
+    y = sub(x, t);
+    x = add(x, t);
+  } else {
+    felt d = sub(x, y);
+    x = add(x, y);
+    y = mul(d, w);
+  }
+}
+
+template <bool DIT, int NT>
+__global__ __launch_bounds__(NT) void k_ntt8(Ntt8Args a) {
+  constexpr int E = NT * 8;
+  extern __shared__ felt lds[];
+  const uint32_t T = 1u << a.logT, Tl = 1u << a.logTl, K = a.K, lo = a.lo;
+  const uint32_t TP = T + 1;  // padded LDS row (bank spread)
+  const uint32_t bidx = blockIdx.y;
+  const felt* src = a.src + (uint64_t)(bidx / a.src_div) * a.src_stride;
+  felt* dst = a.dst + (uint64_t)bidx * a.dst_stride;
+  const felt* scale = a.scale ? a.scale + ((uint64_t)(bidx % a.scale_mod) << a.logn) : nullptr;
+  const uint64_t g0 = (uint64_t)blockIdx.x << a.logT;
+  const uint64_t hi0 = g0 >> lo;
+  const uint64_t l0 = (Tl == T) ? (g0 & ((1ull << lo) - 1)) : 0;
+  const uint32_t qmask = (1u << K) - 1;
+  const uint32_t tid = threadIdx.x;
+  constexpr uint32_t LOGNT = NT == 1024 ? 10 : (NT == 512 ? 9 : 8);
+
+  // coalesced global -> LDS (element order: ll fastest, then q, then hl)
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    uint32_t e = tid + i * NT;
+    uint32_t ll = e & (Tl - 1);
+    uint32_t rest = e >> a.logTl;
+    uint32_t q = rest & qmask;
+    uint32_t hl = rest >> K;
+    uint64_t addr = ((hi0 + hl) << (lo + K)) + ((uint64_t)q << lo) + l0 + ll;
+    felt v = src[addr];
+    if (scale) v = mul(v, scale[addr]);
+    lds[q * TP + (hl * Tl + ll)] = v;
+  }
+
+  uint32_t b0 = DIT ? 0 : K;
+  for (uint32_t r = 0; r < a.nrounds; r++) {
+    const uint32_t rb = a.rbits[r];
+    if (!DIT) b0 -= rb;
+    __syncthreads();
+    felt x[8];
+    uint32_t idx[8];
+    uint32_t ggs[2], qlow[2];
+#pragma unroll
+    for (int m = 0; m < 8; m++) {
+      uint32_t extra = m >> rb, bf = m & ((1u << rb) - 1);
+      uint32_t c = (extra << LOGNT) | tid;
+      uint32_t gg = c & (T - 1);
+      uint32_t qo = c >> a.logT;
+      uint32_t ql = qo & ((1u << b0) - 1);
+      uint32_t q = ((qo >> b0) << (b0 + rb)) | (bf << b0) | ql;
+      idx[m] = q * TP + gg;
+      x[m] = lds[idx[m]];
+      if (bf == 0 && extra < 2) { ggs[extra] = gg; qlow[extra] = ql; }
+    }
+    if (rb == 3) {
+      const uint64_t l = l0 + (ggs[0] & (Tl - 1));
+      const uint64_t jb = ((uint64_t)qlow[0] << lo) | l;
+      felt w0 = ntt_tw<DIT>(a, jb, b0);
+      felt w1a = ntt_tw<DIT>(a, jb, b0 + 1), w1b = ntt_tw<DIT>(a, jb | (1ull << (b0 + lo)), b0 + 1);
+      felt w2[4];
+#pragma unroll
+      for (int k2 = 0; k2 < 4; k2++) w2[k2] = ntt_tw<DIT>(a, jb | ((uint64_t)k2 << (b0 + lo)), b0 + 2);
+      if (DIT) {
+        bfly<true>(x[0], x[1], w0); bfly<true>(x[2], x[3], w0); bfly<true>(x[4], x[5], w0); bfly<true>(x[6], x[7], w0);
+        bfly<true>(x[0], x[2], w1a); bfly<true>(x[1], x[3], w1b); bfly<true>(x[4], x[6], w1a); bfly<true>(x[5], x[7], w1b);
+        bfly<true>(x[0], x[4], w2[0]); bfly<true>(x[1], x[5], w2[1]); bfly<true>(x[2], x[6], w2[2]); bfly<true>(x[3], x[7], w2[3]);
+      } else {
+        bfly<false>(x[0], x[4], w2[0]); bfly<false>(x[1], x[5], w2[1]); bfly<false>(x[2], x[6], w2[2]); bfly<false>(x[3], x[7], w2[3]);
+        bfly<false>(x[0], x[2], w1a); bfly<false>(x[1], x[3], w1b); bfly<false>(x[4], x[6], w1a); bfly<false>(x[5], x[7], w1b);
+        bfly<false>(x[0], x[1], w0); bfly<false>(x[2], x[3], w0); bfly<false>(x[4], x[5], w0); bfly<false>(x[6], x[7], w0);
+      }
+    } else if (rb == 2) {
+#pragma unroll
+      for (int u = 0; u < 2; u++) {
+        const uint64_t l = l0 + (ggs[u] & (Tl - 1));
+        const uint64_t jb = ((uint64_t)qlow[u] << lo) | l;
+        felt w0 = ntt_tw<DIT>(a, jb, b0);
+        felt w1a = ntt_tw<DIT>(a, jb, b0 + 1), w1b = ntt_tw<DIT>(a, jb | (1ull << (b0 + lo)), b0 + 1);
+        felt* y = x + 4 * u;
+        if (DIT) {
+          bfly<true>(y[0], y[1], w0); bfly<true>(y[2], y[3], w0);
+          bfly<true>(y[0], y[2], w1a); bfly<true>(y[1], y[3], w1b);
+        } else {
+          bfly<false>(y[0], y[2], w1a); bfly<false>(y[1], y[3], w1b);
+          bfly<false>(y[0], y[1], w0); bfly<false>(y[2], y[3], w0);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        uint32_t c = ((uint32_t)u << LOGNT) | tid;
+        uint32_t gg = c & (T - 1);
+        uint32_t ql = (c >> a.logT) & ((1u << b0) - 1);
+        const uint64_t jb = ((uint64_t)ql << lo) | (l0 + (gg & (Tl - 1)));
+        bfly<DIT>(x[2 * u], x[2 * u + 1], ntt_tw<DIT>(a, jb, b0));
+      }
+    }
+#pragma unroll
+    for (int m = 0; m < 8; m++) lds[idx[m]] = x[m];
+    if (DIT) b0 += rb;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    uint32_t e = tid + i * NT;
+    uint32_t ll = e & (Tl - 1);
+    uint32_t rest = e >> a.logTl;
+    uint32_t q = rest & qmask;
+    uint32_t hl = rest >> K;
+    uint64_t addr = ((hi0 + hl) << (lo + K)) + ((uint64_t)q << lo) + l0 + ll;
+    dst[addr] = lds[q * TP + (hl * Tl + ll)];
+  }
+  (void)E;
 }
 
 // ------------------------------------------------------------------ tables
@@ -220,39 +379,122 @@ __global__ __launch_bounds__(TPB) void k_grind(SeedArg seed, uint64_t base, uint
 // -------------------------------------------------------------- constraints
 constexpr int EVAL_CH = 8;  // points per thread (batch-inversion chunk)
 
-__device__ __forceinline__ void batch_inverse(felt* v, int n) {
+// Inverts v[0..EVAL_CH) of every thread of the block given the inverse of the
+// product of all of the block's values (Montgomery's trick over thread-local
+// prefixes + two LDS scans).
+// Entries with k >= cnt must hold 1. Every thread of the block must call it.
+__device__ __forceinline__ void block_batch_inverse(felt* v, felt* s_pre, felt* s_suf, felt block_inv) {
   felt pre[EVAL_CH];
   felt acc = one();
-#pragma unroll
-  for (int i = 0; i < EVAL_CH; i++) {
-    if (i < n) { pre[i] = acc; acc = mul(acc, v[i]); }
+  static_for<0, EVAL_CH>([&](auto i) {
+    pre[i] = acc;
+    acc = mul(acc, v[i]);
+  });
+  const uint32_t t = threadIdx.x;
+  s_pre[t] = acc;
+  s_suf[t] = acc;
+  __syncthreads();
+  // inclusive scans: prefix (from the left) and suffix (from the right)
+  for (uint32_t d = 1; d < TPB; d <<= 1) {
+    felt a = t >= d ? s_pre[t - d] : one();
+    felt b = t + d < TPB ? s_suf[t + d] : one();
+    __syncthreads();
+    s_pre[t] = mul(s_pre[t], a);
+    s_suf[t] = mul(s_suf[t], b);
+    __syncthreads();
   }
-  felt ia = inv(acc);
-#pragma unroll
-  for (int i = EVAL_CH - 1; i >= 0; i--) {
-    if (i < n) {
-      felt t = mul(ia, pre[i]);
-      ia = mul(ia, v[i]);
-      v[i] = t;
+  // inv(acc_t) = inv(total) * prefix_excl(t) * suffix_excl(t); inv(total) was
+  // computed by k_den_products + k_invert_products (one inversion per launch)
+  felt ia = block_inv;
+  if (t > 0) ia = mul(ia, s_pre[t - 1]);
+  if (t + 1 < TPB) ia = mul(ia, s_suf[t + 1]);
+  static_for<0, EVAL_CH>([&](auto ii) {
+    constexpr int i = EVAL_CH - 1 - decltype(ii)::value;
+    felt r = mul(ia, pre[i]);
+    ia = mul(ia, v[i]);
+    v[i] = r;
+  });
+}
+
+// Phase 1 of the split batch inversion: product of the denominators
+// (x_s - c0)(x_s - c1) (or (x_s - c0) when !two) of each block's EVAL_CH*TPB
+// points, x_s = g * w_N^(s << xsh). Same point->block mapping as the phase-3 kernels.
+__global__ __launch_bounds__(TPB) void k_den_products(felt g, const felt* __restrict__ tw, uint32_t logN,
+                                                      uint32_t xsh, uint64_t count, felt c0, felt c1, int two,
+                                                      felt* __restrict__ prod) {
+  __shared__ felt s[TPB];
+  const uint64_t base = (blockIdx.x * (uint64_t)TPB + threadIdx.x) * EVAL_CH;
+  felt acc = one();
+  static_for<0, EVAL_CH>([&](auto k) {
+    if (base + k < count) {
+      felt x = mul(g, tw_full(tw, (base + k) << xsh, logN));
+      felt d = sub(x, c0);
+      if (two) d = mul(d, sub(x, c1));
+      acc = mul(acc, d);
     }
+  });
+  s[threadIdx.x] = acc;
+  __syncthreads();
+  for (uint32_t h = TPB / 2; h >= 1; h >>= 1) {
+    if (threadIdx.x < h) s[threadIdx.x] = mul(s[threadIdx.x], s[threadIdx.x + h]);
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) prod[blockIdx.x] = s[0];
+}
+
+// Phase 2: invert all block products in place with one field inversion.
+__global__ __launch_bounds__(1024) void k_invert_products(felt* prod, uint32_t nb) {
+  __shared__ felt s_pre[1024], s_suf[1024];
+  __shared__ felt s_inv;
+  const uint32_t t = threadIdx.x;
+  const uint32_t per = (nb + 1023) / 1024;
+  felt acc = one();
+  for (uint32_t i = 0; i < per; i++) {
+    uint32_t j = t * per + i;
+    if (j < nb) acc = mul(acc, prod[j]);
+  }
+  s_pre[t] = acc;
+  s_suf[t] = acc;
+  __syncthreads();
+  for (uint32_t d = 1; d < 1024; d <<= 1) {
+    felt a = t >= d ? s_pre[t - d] : one();
+    felt b = t + d < 1024 ? s_suf[t + d] : one();
+    __syncthreads();
+    s_pre[t] = mul(s_pre[t], a);
+    s_suf[t] = mul(s_suf[t], b);
+    __syncthreads();
+  }
+  if (t == 0) s_inv = inv(s_pre[1023]);
+  __syncthreads();
+  felt ia = s_inv;
+  if (t > 0) ia = mul(ia, s_pre[t - 1]);
+  if (t + 1 < 1024) ia = mul(ia, s_suf[t + 1]);
+  // back-substitute this thread's run (recomputing its prefix products)
+  for (uint32_t i = per; i-- > 0;) {
+    uint32_t j = t * per + i;
+    if (j >= nb) continue;
+    felt pre = one();
+    for (uint32_t m = 0; m < i; m++) pre = mul(pre, prod[t * per + m]);
+    felt r = mul(ia, pre);
+    ia = mul(ia, prod[j]);
+    prod[j] = r;
   }
 }
 
 __global__ __launch_bounds__(TPB) void k_eval_mimc(EvalCommon c, MimcEvalArgs a, const felt* __restrict__ lde,
-                                                   felt* __restrict__ comp) {
+                                                   const felt* __restrict__ binv, felt* __restrict__ comp) {
+  __shared__ felt s_pre[TPB], s_suf[TPB];
   const uint64_t M = 1ull << (c.logn + c.logce);
   const uint64_t base = (blockIdx.x * (uint64_t)TPB + threadIdx.x) * EVAL_CH;
-  if (base >= M) return;
-  const int cnt = (int)((M - base) < EVAL_CH ? (M - base) : EVAL_CH);
+  const int cnt = base >= M ? 0 : (int)((M - base) < EVAL_CH ? (M - base) : EVAL_CH);
   const uint64_t n = 1ull << c.logn;
   const uint32_t sh = c.logB - c.logce;
   const uint32_t xsh = c.logN - c.logce - c.logn;
   const uint64_t kmask = (64ull << c.logce) - 1;
   felt tpart[EVAL_CH], bnum[EVAL_CH], den[EVAL_CH];
-#pragma unroll
-  for (int k = 0; k < EVAL_CH; k++) {
-    if (k >= cnt) { den[k] = one(); continue; }
-    uint64_t s = base + k;
+  static_for<0, EVAL_CH>([&](auto k) {
+    const bool valid = k < cnt;
+    uint64_t s = valid ? base + k : 0;
     uint64_t idx = s << sh;
     uint64_t j = idx & ((1ull << c.logB) - 1), t = idx >> c.logB;
     felt cur = lde[j * n + t];
@@ -265,29 +507,28 @@ __global__ __launch_bounds__(TPB) void k_eval_mimc(EvalCommon c, MimcEvalArgs a,
     felt e0 = sub(x, one()), e1 = sub(x, c.w_last);
     tpart[k] = mul(mul(tr, e1), c.zinv[s & ((1ull << c.logce) - 1)]);
     bnum[k] = add(mul(mul(a.b0, sub(cur, a.v0)), e1), mul(mul(a.b1, sub(cur, a.v1)), e0));
-    den[k] = mul(e0, e1);
-  }
-  batch_inverse(den, cnt);
-#pragma unroll
-  for (int k = 0; k < EVAL_CH; k++)
+    den[k] = valid ? mul(e0, e1) : one();
+  });
+  block_batch_inverse(den, s_pre, s_suf, binv[blockIdx.x]);
+  static_for<0, EVAL_CH>([&](auto k) {
     if (k < cnt) comp[base + k] = add(tpart[k], mul(bnum[k], den[k]));
+  });
 }
 
 __global__ __launch_bounds__(TPB) void k_eval_linear(EvalCommon c, LinearEvalArgs a, const felt* __restrict__ lde,
-                                                     felt* __restrict__ comp) {
+                                                     const felt* __restrict__ binv, felt* __restrict__ comp) {
+  __shared__ felt s_pre[TPB], s_suf[TPB];
   const uint64_t M = 1ull << (c.logn + c.logce);
   const uint64_t base = (blockIdx.x * (uint64_t)TPB + threadIdx.x) * EVAL_CH;
-  if (base >= M) return;
-  const int cnt = (int)((M - base) < EVAL_CH ? (M - base) : EVAL_CH);
+  const int cnt = base >= M ? 0 : (int)((M - base) < EVAL_CH ? (M - base) : EVAL_CH);
   const uint64_t n = 1ull << c.logn;
   const uint32_t sh = c.logB - c.logce;
   const uint32_t xsh = c.logN - c.logce - c.logn;
   const uint64_t cstride = n << c.logB;
   felt tpart[EVAL_CH], bnum[EVAL_CH], den[EVAL_CH];
-#pragma unroll
-  for (int k = 0; k < EVAL_CH; k++) {
-    if (k >= cnt) { den[k] = one(); continue; }
-    uint64_t s = base + k;
+  static_for<0, EVAL_CH>([&](auto k) {
+    const bool valid = k < cnt;
+    uint64_t s = valid ? base + k : 0;
     uint64_t idx = s << sh;
     uint64_t j = idx & ((1ull << c.logB) - 1), t = idx >> c.logB;
     const felt* pc = lde + j * n + t;
@@ -301,12 +542,12 @@ __global__ __launch_bounds__(TPB) void k_eval_linear(EvalCommon c, LinearEvalArg
     felt x = mul(c.g, tw_full(c.tw, s << xsh, c.logN));
     tpart[k] = mul(mul(tr, sub(x, c.w_last)), c.zinv[s & ((1ull << c.logce) - 1)]);
     bnum[k] = sub(bs, a.bconst);
-    den[k] = sub(x, a.w_bstep);
-  }
-  batch_inverse(den, cnt);
-#pragma unroll
-  for (int k = 0; k < EVAL_CH; k++)
+    den[k] = valid ? sub(x, a.w_bstep) : one();
+  });
+  block_batch_inverse(den, s_pre, s_suf, binv[blockIdx.x]);
+  static_for<0, EVAL_CH>([&](auto k) {
     if (k < cnt) comp[base + k] = add(tpart[k], mul(bnum[k], den[k]));
+  });
 }
 
 __global__ void k_segment(const felt* __restrict__ difout, uint32_t logn, uint32_t logce, uint32_t C,
@@ -352,18 +593,17 @@ __global__ __launch_bounds__(TPB) void k_eval_bitrev(const felt* __restrict__ ar
   }
 }
 
-__global__ __launch_bounds__(TPB) void k_deep(DeepArgs a, felt* __restrict__ out) {
+__global__ __launch_bounds__(TPB) void k_deep(DeepArgs a, const felt* __restrict__ binv, felt* __restrict__ out) {
+  __shared__ felt s_pre[TPB], s_suf[TPB];
   const uint64_t N = 1ull << a.logN;
   const uint64_t base = (blockIdx.x * (uint64_t)TPB + threadIdx.x) * EVAL_CH;
-  if (base >= N) return;
-  const int cnt = (int)((N - base) < EVAL_CH ? (N - base) : EVAL_CH);
+  const int cnt = base >= N ? 0 : (int)((N - base) < EVAL_CH ? (N - base) : EVAL_CH);
   const uint64_t n = 1ull << a.logn;
   const uint64_t cstride = n << a.logB;
   felt num[EVAL_CH], den[EVAL_CH];
-#pragma unroll
-  for (int k = 0; k < EVAL_CH; k++) {
-    if (k >= cnt) { den[k] = one(); continue; }
-    uint64_t i = base + k;
+  static_for<0, EVAL_CH>([&](auto k) {
+    const bool valid = k < cnt;
+    uint64_t i = valid ? base + k : 0;
     uint64_t j = i & ((1ull << a.logB) - 1), t = i >> a.logB;
     const uint64_t off = j * n + t;
     felt A = zero(), Bh = zero();
@@ -372,12 +612,12 @@ __global__ __launch_bounds__(TPB) void k_deep(DeepArgs a, felt* __restrict__ out
     felt x = mul(a.g, tw_full(a.tw, i, a.logN));
     felt e1 = sub(x, a.z), e2 = sub(x, a.zg);
     num[k] = add(mul(sub(add(A, Bh), a.kz), e2), mul(sub(A, a.kzg), e1));
-    den[k] = mul(e1, e2);
-  }
-  batch_inverse(den, cnt);
-#pragma unroll
-  for (int k = 0; k < EVAL_CH; k++)
+    den[k] = valid ? mul(e1, e2) : one();
+  });
+  block_batch_inverse(den, s_pre, s_suf, binv[blockIdx.x]);
+  static_for<0, EVAL_CH>([&](auto k) {
     if (k < cnt) out[base + k] = mul(num[k], den[k]);
+  });
 }
 
 // fold-by-16: u = iDFT16(row) (unscaled), result = (1/16) sum_k u_k beta^k,
@@ -390,27 +630,55 @@ __global__ __launch_bounds__(TPB) void k_fri_fold16(const felt* __restrict__ E, 
   felt v[16];
 #pragma unroll
   for (int k = 0; k < 16; k++) v[k] = E[r + k * R];
-  // Gentleman-Sande, natural in -> bit-reversed out
+  // Gentleman-Sande, natural in -> bit-reversed out (fully unrolled, constant indices)
 #pragma unroll
-  for (int half = 8; half >= 1; half >>= 1) {
+  for (int i = 0; i < 8; i++) {
+    felt x = v[i], y = v[i + 8];
+    v[i] = add(x, y);
+    v[i + 8] = i == 0 ? sub(x, y) : mul(sub(x, y), eps_inv[i]);
+  }
 #pragma unroll
-    for (int blk = 0; blk < 16; blk += 2 * half) {
+  for (int blk = 0; blk < 16; blk += 8) {
 #pragma unroll
-      for (int i = 0; i < half; i++) {
-        felt x = v[blk + i], y = v[blk + i + half];
-        v[blk + i] = add(x, y);
-        felt d = sub(x, y);
-        const int m = i * (8 / half);
-        v[blk + i + half] = m == 0 ? d : mul(d, eps_inv[m]);
-      }
+    for (int i = 0; i < 4; i++) {
+      felt x = v[blk + i], y = v[blk + i + 4];
+      v[blk + i] = add(x, y);
+      v[blk + i + 4] = i == 0 ? sub(x, y) : mul(sub(x, y), eps_inv[2 * i]);
     }
+  }
+#pragma unroll
+  for (int blk = 0; blk < 16; blk += 4) {
+    felt x0 = v[blk], y0 = v[blk + 2], x1 = v[blk + 1], y1 = v[blk + 3];
+    v[blk] = add(x0, y0);
+    v[blk + 2] = sub(x0, y0);
+    v[blk + 1] = add(x1, y1);
+    v[blk + 3] = mul(sub(x1, y1), eps_inv[4]);
+  }
+#pragma unroll
+  for (int blk = 0; blk < 16; blk += 2) {
+    felt x = v[blk], y = v[blk + 1];
+    v[blk] = add(x, y);
+    v[blk + 1] = sub(x, y);
   }
   felt beta = mul(alpha, mul(off_inv, itw[r << xsh]));
   // Horner over k = 15..0 with u_k = v[rev4(k)]
-  const int rev4[16] = {0, 8, 4, 12, 2, 10, 6, 14, 1, 9, 5, 13, 3, 11, 7, 15};
-  felt acc = v[rev4[15]];
-#pragma unroll
-  for (int k = 14; k >= 0; k--) acc = add(mul(acc, beta), v[rev4[k]]);
+  // u_k = v[rev4(k)], rev4 = {0,8,4,12,2,10,6,14,1,9,5,13,3,11,7,15}
+  felt acc = v[15];
+  acc = add(mul(acc, beta), v[7]);
+  acc = add(mul(acc, beta), v[11]);
+  acc = add(mul(acc, beta), v[3]);
+  acc = add(mul(acc, beta), v[13]);
+  acc = add(mul(acc, beta), v[5]);
+  acc = add(mul(acc, beta), v[9]);
+  acc = add(mul(acc, beta), v[1]);
+  acc = add(mul(acc, beta), v[14]);
+  acc = add(mul(acc, beta), v[6]);
+  acc = add(mul(acc, beta), v[10]);
+  acc = add(mul(acc, beta), v[2]);
+  acc = add(mul(acc, beta), v[12]);
+  acc = add(mul(acc, beta), v[4]);
+  acc = add(mul(acc, beta), v[8]);
+  acc = add(mul(acc, beta), v[0]);
   out[r] = mul(acc, eps_inv[8]);
 }
 
@@ -504,8 +772,8 @@ std::vector<NttPass> ntt_plan(uint32_t logn, bool dit) {
   return out;
 }
 
-void launch_ntt(Prof& prof, hipStream_t s, const NttBatch& b, uint32_t logn, bool dit, const felt* tw,
-                uint32_t logN) {
+static void launch_ntt_radix2(Prof& prof, hipStream_t s, const NttBatch& b, uint32_t logn, bool dit,
+                              const felt* tw, uint32_t logN) {
   auto plan = ntt_plan(logn, dit);
   bool first = true;
   for (const auto& ps : plan) {
@@ -531,9 +799,70 @@ void launch_ntt(Prof& prof, hipStream_t s, const NttBatch& b, uint32_t logn, boo
     uint64_t groups = 1ull << (logn - ps.K);
     dim3 grid((uint32_t)(groups / ps.T), b.batches);
     size_t shmem = (size_t)(ps.T << ps.K) * sizeof(felt);
-    LAUNCH(prof, dit ? "ntt_dit_pass" : "ntt_dif_pass", s, (double)b.batches * (1ull << logn) * 16.0 * (a.scale ? 3 : 2),
+    LAUNCH(prof, dit ? "ntt_dit_r2" : "ntt_dif_r2", s, (double)b.batches * (1ull << logn) * 16.0 * (a.scale ? 3 : 2),
            hipLaunchKernelGGL(k_ntt_pass, grid, dim3(TPB), shmem, s, a));
     first = false;
+  }
+}
+
+// radix-8 register-blocked passes: 256-thread blocks (E = 2048 elements, K <= 8)
+// for the big transforms (several blocks per CU overlap load and compute);
+// n must be >= 2^11.
+void launch_ntt(Prof& prof, hipStream_t s, const NttBatch& b, uint32_t logn, bool dit, const felt* tw,
+                uint32_t logN) {
+  const uint32_t LOGE = 11, KMAX = 8;
+  if (logn < LOGE) {
+    launch_ntt_radix2(prof, s, b, logn, dit, tw, logN);
+    return;
+  }
+  uint32_t npass = (logn + KMAX - 1) / KMAX;
+  static bool attr_set = false;
+  if (!attr_set) {
+    size_t maxb = (size_t)(1u << LOGE) * (1 + 1.0 / 8) * sizeof(felt) + 16;
+    (void)hipFuncSetAttribute((const void*)k_ntt8<true, 256>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)maxb);
+    (void)hipFuncSetAttribute((const void*)k_ntt8<false, 256>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)maxb);
+    attr_set = true;
+  }
+  uint32_t s0 = 0;
+  for (uint32_t p = 0; p < npass; p++) {
+    uint32_t K = logn / npass + (p < logn % npass ? 1 : 0);
+    Ntt8Args a;
+    bool first = p == 0;
+    a.src = first ? b.src : b.dst;
+    a.dst = b.dst;
+    a.scale = first ? b.scale : nullptr;
+    a.tw = tw;
+    a.src_stride = first ? b.src_stride : b.dst_stride;
+    a.dst_stride = b.dst_stride;
+    a.src_div = first ? b.src_div : 1;
+    a.scale_mod = b.scale_mod ? b.scale_mod : 1;
+    a.logn = logn;
+    a.s0 = s0;
+    a.K = K;
+    a.lo = dit ? s0 : logn - s0 - K;
+    a.logT = LOGE - K;
+    a.logTl = a.logT < a.lo ? a.logT : a.lo;
+    a.tw_shift = logN - logn;
+    // rounds of <= 3 bits, larger first
+    uint32_t nr = (K + 2) / 3, rem = K;
+    a.nrounds = nr;
+    for (uint32_t r = 0; r < 4; r++) a.rbits[r] = 0;
+    for (uint32_t r = 0; r < nr; r++) {
+      uint32_t rb = rem / (nr - r) + (rem % (nr - r) ? 1 : 0);
+      if (rb > 3) rb = 3;
+      a.rbits[r] = rb;
+      rem -= rb;
+    }
+    uint64_t groups = 1ull << (logn - K);
+    dim3 grid((uint32_t)(groups >> a.logT), b.batches);
+    size_t shmem = (size_t)(1u << K) * ((1u << a.logT) + 1) * sizeof(felt);
+    if (dit)
+      LAUNCH(prof, "ntt_dit", s, (double)b.batches * (1ull << logn) * 16.0 * (a.scale ? 3 : 2),
+             hipLaunchKernelGGL((k_ntt8<true, 256>), grid, dim3(256), shmem, s, a));
+    else
+      LAUNCH(prof, "ntt_dif", s, (double)b.batches * (1ull << logn) * 16.0 * (a.scale ? 3 : 2),
+             hipLaunchKernelGGL((k_ntt8<false, 256>), grid, dim3(256), shmem, s, a));
+    s0 += K;
   }
 }
 
@@ -585,20 +914,33 @@ void launch_grind(Prof& prof, hipStream_t s, const uint32_t* seed_words, uint64_
          hipLaunchKernelGGL(k_grind, dim3(blocks_for(count)), dim3(TPB), 0, s, sa, base, count, bits, result));
 }
 
+static void launch_den_inverse(Prof& prof, hipStream_t s, felt g, const felt* tw, uint32_t logN, uint32_t xsh,
+                               uint64_t count, felt c0, felt c1, int two, felt* prod) {
+  uint32_t nb = blocks_for((count + EVAL_CH - 1) / EVAL_CH);
+  LAUNCH(prof, "den_products", s, (double)count * 16.0,
+         hipLaunchKernelGGL(k_den_products, dim3(nb), dim3(TPB), 0, s, g, tw, logN, xsh, count, c0, c1, two, prod));
+  LAUNCH(prof, "invert_products", s, (double)nb * 32.0,
+         hipLaunchKernelGGL(k_invert_products, dim3(1), dim3(1024), 0, s, prod, nb));
+}
+
 void launch_eval_mimc(Prof& prof, hipStream_t s, const EvalCommon& c, const MimcEvalArgs& a, const felt* lde,
                       felt* comp) {
   uint64_t M = 1ull << (c.logn + c.logce);
+  if (!a.binv_ready)
+    launch_den_inverse(prof, s, c.g, c.tw, c.logN, c.logN - c.logce - c.logn, M, one(), c.w_last, 1, a.binv);
   LAUNCH(prof, "eval_mimc", s, (double)M * 32.0,
          hipLaunchKernelGGL(k_eval_mimc, dim3(blocks_for((M + EVAL_CH - 1) / EVAL_CH)), dim3(TPB), 0, s, c, a, lde,
-                            comp));
+                            a.binv, comp));
 }
 
 void launch_eval_linear(Prof& prof, hipStream_t s, const EvalCommon& c, const LinearEvalArgs& a, const felt* lde,
                         felt* comp) {
   uint64_t M = 1ull << (c.logn + c.logce);
+  if (!a.binv_ready)
+    launch_den_inverse(prof, s, c.g, c.tw, c.logN, c.logN - c.logce - c.logn, M, a.w_bstep, zero(), 0, a.binv);
   LAUNCH(prof, "eval_linear", s, (double)M * (a.width * 16.0 + 16.0),
          hipLaunchKernelGGL(k_eval_linear, dim3(blocks_for((M + EVAL_CH - 1) / EVAL_CH)), dim3(TPB), 0, s, c, a, lde,
-                            comp));
+                            a.binv, comp));
 }
 
 void launch_segment(Prof& prof, hipStream_t s, const felt* difout, uint32_t logn, uint32_t logce, uint32_t C,
@@ -620,8 +962,9 @@ void launch_eval_bitrev(Prof& prof, hipStream_t s, const felt* arrays, uint32_t 
 
 void launch_deep(Prof& prof, hipStream_t s, const DeepArgs& a, felt* out) {
   uint64_t N = 1ull << a.logN;
+  launch_den_inverse(prof, s, a.g, a.tw, a.logN, 0, N, a.z, a.zg, 1, a.binv);
   LAUNCH(prof, "deep", s, (double)N * ((a.w + a.C) * 16.0 + 16.0),
-         hipLaunchKernelGGL(k_deep, dim3(blocks_for((N + EVAL_CH - 1) / EVAL_CH)), dim3(TPB), 0, s, a, out));
+         hipLaunchKernelGGL(k_deep, dim3(blocks_for((N + EVAL_CH - 1) / EVAL_CH)), dim3(TPB), 0, s, a, a.binv, out));
 }
 
 void launch_fri_fold(Prof& prof, hipStream_t s, const felt* E, uint64_t R, uint32_t F, felt alpha, felt off_inv,

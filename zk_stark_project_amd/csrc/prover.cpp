@@ -357,6 +357,13 @@ struct zkp_ctx {
     return reinterpret_cast<T*>(b.p);
   }
   void sync() { HIP_CHECK(hipStreamSynchronize(stream)); }
+  // true if `key` was already produced by an earlier call (the caller fills it otherwise)
+  std::map<std::string, bool> cached;
+  bool have_cached(const std::string& key) {
+    bool had = cached[key];
+    cached[key] = true;
+    return had;
+  }
   void upload(void* d, const void* h, size_t bytes) {
     HIP_CHECK(hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, stream));
   }
@@ -585,6 +592,10 @@ int prove_impl(zkp_ctx* ctx, int air_id, const felt* d_trace, uint32_t w, uint64
       ma.b0 = cc[1]; ma.v0 = air.a_val[0];
       ma.b1 = cc[2]; ma.v1 = air.a_val[1];
       ma.kper = dk;
+      // divisor inverses depend only on the domain and the assertion steps: cache per config
+      std::string key = "binv_mimc_" + std::to_string(logn) + "_" + std::to_string(logB);
+      ma.binv_ready = ctx->have_cached(key);
+      ma.binv = ctx->buf<felt>(key, M / 2048 + 1);
       launch_eval_mimc(pf, st, ec, ma, tlde, comp);
     } else {
       // GlobalUpdate: T = sum_i a^i (k*next_i - k*cur_i - next_{i+60}); B = sum_c b_c (cur_c - v_c)
@@ -606,6 +617,10 @@ int prove_impl(zkp_ctx* ctx, int air_id, const felt* d_trace, uint32_t w, uint64
       la.coefs = dco;
       la.bconst = bconst;
       la.w_bstep = pow_u64(wn, air.a_step[0]);
+      std::string key = "binv_lin_" + std::to_string(logn) + "_" + std::to_string(logB) + "_" +
+                        std::to_string(air.a_step[0]);
+      la.binv_ready = ctx->have_cached(key);
+      la.binv = ctx->buf<felt>(key, M / 2048 + 1);
       launch_eval_linear(pf, st, ec, la, tlde, comp);
     }
   }
@@ -658,6 +673,7 @@ int prove_impl(zkp_ctx* ctx, int air_id, const felt* d_trace, uint32_t w, uint64
     da.tlde = tlde; da.clde = clde; da.gamma = dg2;
     da.z = z; da.zg = zg; da.kz = kz; da.kzg = kzg; da.g = g;
     da.tw = ctx->tw(logN);
+    da.binv = ctx->buf<felt>("binv", N / 2048 + 1);
     launch_deep(pf, st, da, deep);
   }
 

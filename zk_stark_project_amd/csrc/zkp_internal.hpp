@@ -78,6 +78,8 @@ struct EvalCommon {
 struct MimcEvalArgs {
   felt coef_t, b0, b1, v0, v1;
   const felt* kper;      // 64*ce periodic values on the CE domain
+  felt* binv;            // one felt per 2048 CE points (per-block inverse products)
+  bool binv_ready;       // binv already holds this domain's values (cached in the ctx)
 };
 void launch_eval_mimc(Prof& prof, hipStream_t s, const EvalCommon& c, const MimcEvalArgs& a, const felt* lde,
                       felt* comp);
@@ -87,6 +89,8 @@ struct LinearEvalArgs {
   uint32_t width;
   const felt* coefs;     // 3*width: a_c, b_c, beta_c
   felt bconst, w_bstep;
+  felt* binv;            // one felt per 2048 CE points
+  bool binv_ready;
 };
 void launch_eval_linear(Prof& prof, hipStream_t s, const EvalCommon& c, const LinearEvalArgs& a, const felt* lde,
                         felt* comp);
@@ -108,6 +112,7 @@ struct DeepArgs {
   const felt* gamma;     // w + C
   felt z, zg, kz, kzg, g;
   const felt* tw;
+  felt* binv;            // scratch: one felt per 2048 LDE points
 };
 void launch_deep(Prof& prof, hipStream_t s, const DeepArgs& a, felt* out);
 
