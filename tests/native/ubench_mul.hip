@@ -62,6 +62,9 @@ __global__ void k_bench(felt* io, int iters) {
     if (V == 6) { x0 = fpd::mul(x0, y); x1 = fpd::mul(x1, y); x2 = fpd::mul(x2, y); x3 = fpd::mul(x3, y); }
     if (V == 7) { x0 = fpd::add(x0, y); x1 = fpd::add(x1, y); x2 = fpd::add(x2, y); x3 = fpd::add(x3, y); }
     if (V == 8) { x0 = sub(x0, y); x1 = sub(x1, y); x2 = sub(x2, y); x3 = sub(x3, y); }
+    if (V == 10) { fpd::mul_x2(x0, y, x1, y, x0, x1); fpd::mul_x2(x2, y, x3, y, x2, x3); }
+    if (V == 11) { felt s0, d0, s1, d1; fpd::addsub(x0, x1, s0, d0); fpd::addsub(x2, x3, s1, d1); x0 = s0; x1 = d0; x2 = s1; x3 = d1; }
+    if (V == 12) { felt s0, d0, s1, d1; s0 = add(x0, x1); d0 = sub(x0, x1); s1 = add(x2, x3); d1 = sub(x2, x3); x0 = s0; x1 = d0; x2 = s1; x3 = d1; }
     if (V == 9) { x0 = fpd::sub(x0, y); x1 = fpd::sub(x1, y); x2 = fpd::sub(x2, y); x3 = fpd::sub(x3, y); }
   }
   io[4 * t] = x0; io[4 * t + 1] = x1; io[4 * t + 2] = x2; io[4 * t + 3] = x3;
@@ -115,6 +118,9 @@ int main() {
   run("mul v2 (u128 products)", [&] { hipLaunchKernelGGL(k_bench<2>, dim3(blocks), dim3(tpb), 0, 0, d, iters); }, 4);
   run("mul v3 (product scan)", [&] { hipLaunchKernelGGL(k_bench<3>, dim3(blocks), dim3(tpb), 0, 0, d, iters); }, 4);
   run("mul v6 (asm carry chains)", [&] { hipLaunchKernelGGL(k_bench<6>, dim3(blocks), dim3(tpb), 0, 0, d, iters); }, 4);
+  run("mul x2 interleaved", [&] { hipLaunchKernelGGL(k_bench<10>, dim3(blocks), dim3(tpb), 0, 0, d, iters); }, 4);
+  run("addsub interleaved", [&] { hipLaunchKernelGGL(k_bench<11>, dim3(blocks), dim3(tpb), 0, 0, d, iters); }, 4);
+  run("add+sub separate", [&] { hipLaunchKernelGGL(k_bench<12>, dim3(blocks), dim3(tpb), 0, 0, d, iters); }, 4);
   run("add asm", [&] { hipLaunchKernelGGL(k_bench<7>, dim3(blocks), dim3(tpb), 0, 0, d, iters); }, 4);
   run("sub", [&] { hipLaunchKernelGGL(k_bench<8>, dim3(blocks), dim3(tpb), 0, 0, d, iters); }, 4);
   run("sub asm", [&] { hipLaunchKernelGGL(k_bench<9>, dim3(blocks), dim3(tpb), 0, 0, d, iters); }, 4);
@@ -140,7 +146,7 @@ int main() {
       if (ge_p(v)) v = make(lo - 0xffffd30000000001ULL, 0);  // keep canonical
       h0[i] = v;
     }
-    int pairs[4][2] = {{1, 2}, {1, 6}, {5, 7}, {8, 9}};
+    int pairs[6][2] = {{1, 2}, {1, 6}, {5, 7}, {8, 9}, {1, 10}, {12, 11}};
     for (auto& pr : pairs) {
       felt* outs[2] = {h1, h2};
       for (int k = 0; k < 2; k++) {
@@ -153,6 +159,9 @@ int main() {
         if (v == 7) hipLaunchKernelGGL(k_bench<7>, dim3(16), dim3(256), 0, 0, a, 3);
         if (v == 8) hipLaunchKernelGGL(k_bench<8>, dim3(16), dim3(256), 0, 0, a, 3);
         if (v == 9) hipLaunchKernelGGL(k_bench<9>, dim3(16), dim3(256), 0, 0, a, 3);
+        if (v == 10) hipLaunchKernelGGL(k_bench<10>, dim3(16), dim3(256), 0, 0, a, 3);
+        if (v == 11) hipLaunchKernelGGL(k_bench<11>, dim3(16), dim3(256), 0, 0, a, 3);
+        if (v == 12) hipLaunchKernelGGL(k_bench<12>, dim3(16), dim3(256), 0, 0, a, 3);
         hipMemcpy(outs[k], a, cnt * sizeof(felt), hipMemcpyDeviceToHost);
       }
       printf("variant %d agrees with %d: %s\n", pr[1], pr[0], memcmp(h1, h2, cnt * sizeof(felt)) == 0 ? "yes" : "NO");

@@ -216,4 +216,147 @@ __device__ __forceinline__ felt mul(felt a, felt b) {
   return reduce(r);
 }
 
+
+// Two independent products with their instruction streams interleaved, so that
+// each SGPR carry is consumed >= 2 instructions after it is produced (gfx950
+// needs 2 wait states between a VALU carry-out and its VALU consumer; with
+// one chain the compiler pads with s_nop).
+__device__ __forceinline__ void mul256x2(L4 x, L4 y, L4 u, L4 v, uint32_t r[8], uint32_t s[8]) {
+  uint64_t acc, c, bcc, d;
+  uint32_t ov, bov;
+  acc = mad(x.w0, y.w0, 0ull);
+  bcc = mad(u.w0, v.w0, 0ull);
+  r[0] = (uint32_t)acc; acc >>= 32;
+  s[0] = (uint32_t)bcc; bcc >>= 32;
+#define ZKP_COL_BEGIN(i0, j0)                      \
+  acc = mad_co(x.w##i0, y.w##j0, acc, c);          \
+  bcc = mad_co(u.w##i0, v.w##j0, bcc, d);          \
+  ov = addc(0u, 0u, c);                            \
+  bov = addc(0u, 0u, d);
+#define ZKP_COL_STEP(i0, j0)                       \
+  acc = mad_co(x.w##i0, y.w##j0, acc, c);          \
+  bcc = mad_co(u.w##i0, v.w##j0, bcc, d);          \
+  ov = addc(ov, 0u, c);                            \
+  bov = addc(bov, 0u, d);
+#define ZKP_COL_END(k)                             \
+  r[k] = (uint32_t)acc;                            \
+  s[k] = (uint32_t)bcc;                            \
+  acc = (acc >> 32) | ((uint64_t)ov << 32);        \
+  bcc = (bcc >> 32) | ((uint64_t)bov << 32);
+  ZKP_COL_BEGIN(0, 1) ZKP_COL_STEP(1, 0) ZKP_COL_END(1)
+  ZKP_COL_BEGIN(0, 2) ZKP_COL_STEP(1, 1) ZKP_COL_STEP(2, 0) ZKP_COL_END(2)
+  ZKP_COL_BEGIN(0, 3) ZKP_COL_STEP(1, 2) ZKP_COL_STEP(2, 1) ZKP_COL_STEP(3, 0) ZKP_COL_END(3)
+  ZKP_COL_BEGIN(1, 3) ZKP_COL_STEP(2, 2) ZKP_COL_STEP(3, 1) ZKP_COL_END(4)
+  ZKP_COL_BEGIN(2, 3) ZKP_COL_STEP(3, 2) ZKP_COL_END(5)
+#undef ZKP_COL_BEGIN
+#undef ZKP_COL_STEP
+#undef ZKP_COL_END
+  acc = mad(x.w3, y.w3, acc);
+  bcc = mad(u.w3, v.w3, bcc);
+  r[6] = (uint32_t)acc; r[7] = (uint32_t)(acc >> 32);
+  s[6] = (uint32_t)bcc; s[7] = (uint32_t)(bcc >> 32);
+}
+
+// Two independent reductions, interleaved like mul256x2.
+__device__ __forceinline__ void reduce_x2(const uint32_t r[8], const uint32_t s[8], felt& out_r, felt& out_s) {
+  const uint32_t K = 0x2d00u;
+  uint64_t t = mad(r[4], K, 0ull), tt = mad(s[4], K, 0ull);
+  uint32_t q0 = (uint32_t)t, p0 = (uint32_t)tt;
+  t = mad(r[5], K, t >> 32); tt = mad(s[5], K, tt >> 32);
+  uint32_t q1 = (uint32_t)t, p1 = (uint32_t)tt;
+  t = mad(r[6], K, t >> 32); tt = mad(s[6], K, tt >> 32);
+  uint32_t q2 = (uint32_t)t, p2 = (uint32_t)tt;
+  t = mad(r[7], K, t >> 32); tt = mad(s[7], K, tt >> 32);
+  uint32_t q3 = (uint32_t)t, q4 = (uint32_t)(t >> 32), p3 = (uint32_t)tt, p4 = (uint32_t)(tt >> 32);
+  uint64_t c, e, b, f;
+  uint32_t s1 = add_co(r[1], q0, c);
+  uint32_t S1 = add_co(s[1], p0, e);
+  uint32_t x0 = sub_co(r[0], r[4], b);
+  uint32_t X0 = sub_co(s[0], s[4], f);
+  uint32_t s2 = addc_co(r[2], q1, c, c);
+  uint32_t S2 = addc_co(s[2], p1, e, e);
+  uint32_t x1 = subb_co(s1, r[5], b, b);
+  uint32_t X1 = subb_co(S1, s[5], f, f);
+  uint32_t s3 = addc_co(r[3], q2, c, c);
+  uint32_t S3 = addc_co(s[3], p2, e, e);
+  uint32_t x2 = subb_co(s2, r[6], b, b);
+  uint32_t X2 = subb_co(S2, s[6], f, f);
+  uint32_t s4 = addc_co(q3, 0u, c, c);
+  uint32_t S4 = addc_co(p3, 0u, e, e);
+  uint32_t x3 = subb_co(s3, r[7], b, b);
+  uint32_t X3 = subb_co(S3, s[7], f, f);
+  uint32_t s5 = addc(q4, 0u, c);
+  uint32_t S5 = addc(p4, 0u, e);
+  uint32_t x4 = subb_co(s4, 0u, b, b);
+  uint32_t X4 = subb_co(S4, 0u, f, f);
+  uint32_t x5 = subb(s5, 0u, b);
+  uint32_t X5 = subb(S5, 0u, f);
+  uint64_t uu = mad(x4, K, 0ull), UU = mad(X4, K, 0ull);
+  uint32_t u0 = (uint32_t)uu, U0 = (uint32_t)UU;
+  uint32_t u1 = (uint32_t)(uu >> 32) + x5 * K, U1 = (uint32_t)(UU >> 32) + X5 * K;
+  uint32_t y1 = add_co(x1, u0, c);
+  uint32_t Y1 = add_co(X1, U0, e);
+  uint32_t z0 = sub_co(x0, x4, b);
+  uint32_t Z0 = sub_co(X0, X4, f);
+  uint32_t y2 = addc_co(x2, u1, c, c);
+  uint32_t Y2 = addc_co(X2, U1, e, e);
+  uint32_t z1 = subb_co(y1, x5, b, b);
+  uint32_t Z1 = subb_co(Y1, X5, f, f);
+  uint32_t y3 = addc_co(x3, 0u, c, c);
+  uint32_t Y3 = addc_co(X3, 0u, e, e);
+  uint32_t z2 = subb_co(y2, 0u, b, b);
+  uint32_t Z2 = subb_co(Y2, 0u, f, f);
+  uint32_t z3 = subb_co(y3, 0u, b, b);
+  uint32_t Z3 = subb_co(Y3, 0u, f, f);
+  uint64_t k1, k2;
+  asm("s_andn2_b64 %0, %1, %2" : "=s"(k1) : "s"(c), "s"(b) : "scc");
+  asm("s_andn2_b64 %0, %1, %2" : "=s"(k2) : "s"(e), "s"(f) : "scc");
+  // canonicalize both (interleaved)
+  uint64_t g1, g2;
+  uint32_t t0 = add_co(z0, C0, g1);
+  uint32_t T0 = add_co(Z0, C0, g2);
+  uint32_t t1 = addc_co(z1, C1, g1, g1);
+  uint32_t T1 = addc_co(Z1, C1, g2, g2);
+  uint32_t t2 = addc_co(z2, 0u, g1, g1);
+  uint32_t T2 = addc_co(Z2, 0u, g2, g2);
+  uint32_t t3 = addc_co(z3, 0u, g1, g1);
+  uint32_t T3 = addc_co(Z3, 0u, g2, g2);
+  uint64_t m1 = or_mask(k1, g1), m2 = or_mask(k2, g2);
+  out_r = join(sel(z0, t0, m1), sel(z1, t1, m1), sel(z2, t2, m1), sel(z3, t3, m1));
+  out_s = join(sel(Z0, T0, m2), sel(Z1, T1, m2), sel(Z2, T2, m2), sel(Z3, T3, m2));
+}
+
+__device__ __forceinline__ void mul_x2(felt a, felt b, felt c, felt d, felt& ab, felt& cd) {
+  uint32_t r[8], s[8];
+  mul256x2(split(a), split(b), split(c), split(d), r, s);
+  reduce_x2(r, s, ab, cd);
+}
+
+// x + y and x - y with the two carry chains interleaved (the butterfly's add/sub pair)
+__device__ __forceinline__ void addsub(felt a, felt b, felt& sum, felt& diff) {
+  L4 x = split(a), y = split(b);
+  uint64_t c, bw;
+  uint32_t s0 = add_co(x.w0, y.w0, c);
+  uint32_t d0 = sub_co(x.w0, y.w0, bw);
+  uint32_t s1 = addc_co(x.w1, y.w1, c, c);
+  uint32_t d1 = subb_co(x.w1, y.w1, bw, bw);
+  uint32_t s2 = addc_co(x.w2, y.w2, c, c);
+  uint32_t d2 = subb_co(x.w2, y.w2, bw, bw);
+  uint32_t s3 = addc_co(x.w3, y.w3, c, c);
+  uint32_t d3 = subb_co(x.w3, y.w3, bw, bw);
+  uint64_t g, b2;
+  uint32_t m0 = sel(0u, C0, bw), m1 = sel(0u, C1, bw);
+  uint32_t t0 = add_co(s0, C0, g);
+  uint32_t e0 = sub_co(d0, m0, b2);
+  uint32_t t1 = addc_co(s1, C1, g, g);
+  uint32_t e1 = subb_co(d1, m1, b2, b2);
+  uint32_t t2 = addc_co(s2, 0u, g, g);
+  uint32_t e2 = subb_co(d2, 0u, b2, b2);
+  uint32_t t3 = addc_co(s3, 0u, g, g);
+  uint32_t e3 = subb(d3, 0u, b2);
+  uint64_t m = or_mask(c, g);
+  sum = join(sel(s0, t0, m), sel(s1, t1, m), sel(s2, t2, m), sel(s3, t3, m));
+  diff = join(e0, e1, e2, e3);
+}
+
 }  // namespace fpd

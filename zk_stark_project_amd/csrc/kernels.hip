@@ -91,7 +91,8 @@ __global__ __launch_bounds__(TPB) void k_ntt_pass(NttKArgs a) {
   for (uint32_t ls = 0; ls < K; ls++) {
     const uint32_t s = a.s0 + ls;
     const uint32_t pbit = a.dit ? ls : (K - 1 - ls);
-    const uint32_t twsh = a.dit ? (a.logn - 1 - s + a.tw_shift) : (s + a.tw_shift);
+    const uint32_t lev = a.dit ? s : (a.logn - 1 - s);  // stage-major twiddle level
+    const felt* twl = a.tw + ((1ull << lev) - 1);
     const uint32_t pmask = (1u << pbit) - 1;
     for (uint32_t bf = threadIdx.x; bf < (E >> 1); bf += TPB) {
       uint32_t gg = bf & (T - 1);
@@ -100,7 +101,7 @@ __global__ __launch_bounds__(TPB) void k_ntt_pass(NttKArgs a) {
       uint32_t q2 = q | (1u << pbit);
       uint64_t l = l0 + (gg & (Tl - 1));
       uint64_t j = ((uint64_t)(q & pmask) << lo) | l;
-      felt w = a.tw[j << twsh];
+      felt w = twl[j];
       uint32_t i0 = (q << a.logT) + gg, i1 = (q2 << a.logT) + gg;
       felt x = lds[i0], y = lds[i1];
       if (a.dit) {
@@ -140,11 +141,12 @@ struct Ntt8Args {
   uint32_t rbits[4];
 };
 
+// stage-major twiddles: level t holds w_{2^(t+1)}^j at tw[(2^t - 1) + j]
 template <bool DIT>
 __device__ __forceinline__ felt ntt_tw(const Ntt8Args& a, uint64_t j, uint32_t pbit) {
   uint32_t s = DIT ? a.s0 + pbit : a.s0 + a.K - 1 - pbit;
-  uint32_t sh = DIT ? (a.logn - 1 - s + a.tw_shift) : (s + a.tw_shift);
-  return a.tw[j << sh];
+  uint32_t lev = DIT ? s : a.logn - 1 - s;
+  return a.tw[((1ull << lev) - 1) + j];
 }
 
 template <bool DIT>
@@ -278,6 +280,17 @@ __global__ void k_expand_powers(felt* out, uint64_t count, const felt* lo_tab, c
     out[e] = mul(lo_tab[e & 2047], hi_tab[e >> 11]);
 }
 
+// stage-major table: level t (< top) = top level gathered with stride 2^(top - t)
+__global__ void k_build_levels(felt* tab, uint32_t top) {
+  const felt* topl = tab + ((1ull << top) - 1);
+  uint64_t total = (1ull << top) - 1;  // entries of levels 0..top-1
+  for (uint64_t e = blockIdx.x * (uint64_t)TPB + threadIdx.x; e < total; e += (uint64_t)gridDim.x * TPB) {
+    uint32_t t = 63 - __builtin_clzll(e + 1);
+    uint64_t j = e + 1 - (1ull << t);
+    tab[e] = topl[j << (top - t)];
+  }
+}
+
 __global__ void k_build_coset_scale(felt* S, uint32_t logn, uint32_t B, const felt* tw, uint32_t logN,
                                     const felt* glo, const felt* ghi, felt ninv) {
   uint64_t total = (uint64_t)B << logn;
@@ -349,6 +362,86 @@ __global__ __launch_bounds__(1024) void k_merkle_top(uint32_t* nodes, uint64_t s
     }
     __threadfence_block();
     __syncthreads();
+  }
+}
+
+// Fused Merkle build: each block turns up to 512 consecutive leaves into all
+// 9 levels of their subtree (leaf digests -> subtree root) with the levels
+// held in LDS and every node written once to nodes[] (tree layout: level d of
+// an L-leaf tree at nodes[(L >> d) .. (2L >> d))). MODE 0: leaves = rows of a
+// coset-major LDE matrix; MODE 1: leaves = FRI rows [E[r + k*R]]; MODE 2:
+// leaves already stored in nodes[L..2L).
+struct MerkleArgs {
+  const felt* src;
+  uint64_t n;       // MODE 0: rows per coset
+  uint32_t cols;    // MODE 0: columns; MODE 1: F
+  uint32_t logB;    // MODE 0
+  uint64_t R;       // MODE 1: rows (= leaves)
+  uint32_t* nodes;
+  uint64_t L;       // leaves of this (sub)tree level
+};
+
+template <int MODE>
+__device__ __forceinline__ void merkle_leaf(const MerkleArgs& a, uint64_t i, uint32_t d[8]) {
+  if (MODE == 0) {
+    uint64_t j = i & ((1ull << a.logB) - 1), t = i >> a.logB;
+    const felt* base = a.src + j * a.n + t;
+    const uint64_t cstride = a.n << a.logB;
+    b3::hash_felts([&](uint32_t c) { return base[c * cstride]; }, a.cols, d);
+  } else if (MODE == 1) {
+    b3::hash_felts([&](uint32_t k) { return a.src[i + k * a.R]; }, a.cols, d);
+  } else {
+    load_digest(a.nodes + (a.L + i) * 8, d);
+  }
+}
+
+__device__ __forceinline__ void merge8(const uint32_t l[8], const uint32_t r[8], uint32_t out[8]) {
+  uint32_t m[16];
+#pragma unroll
+  for (int i = 0; i < 8; i++) { m[i] = l[i]; m[8 + i] = r[i]; }
+  b3::set_iv(out);
+  b3::compress(out, m, 0, 64, b3::CHUNK_START | b3::CHUNK_END | b3::ROOT);
+}
+
+template <int MODE>
+__global__ __launch_bounds__(256) void k_merkle_fused(MerkleArgs a) {
+  __shared__ uint32_t sd[256 * 9];
+  const uint32_t t = threadIdx.x;
+  const uint64_t L = a.L;
+  const uint64_t cnt = L < 512 ? L : 512;          // leaves in this block's subtree
+  const uint64_t base = (uint64_t)blockIdx.x * 512;
+  uint32_t m[8];
+  if (2 * t < cnt) {
+    uint32_t d0[8], d1[8];
+    merkle_leaf<MODE>(a, base + 2 * t, d0);
+    merkle_leaf<MODE>(a, base + 2 * t + 1, d1);
+    if (MODE != 2) {
+      store_digest(a.nodes + (L + base + 2 * t) * 8, d0);
+      store_digest(a.nodes + (L + base + 2 * t + 1) * 8, d1);
+    }
+    merge8(d0, d1, m);
+    store_digest(a.nodes + ((L >> 1) + (base >> 1) + t) * 8, m);
+#pragma unroll
+    for (int i = 0; i < 8; i++) sd[t * 9 + i] = m[i];
+  }
+  uint64_t lvl = L >> 1, lbase = base >> 1;
+  for (uint32_t s = (uint32_t)(cnt >> 2); s >= 1; s >>= 1) {
+    __syncthreads();
+    uint32_t o[8];
+    if (t < s) {
+      uint32_t l[8], r[8];
+#pragma unroll
+      for (int i = 0; i < 8; i++) { l[i] = sd[(2 * t) * 9 + i]; r[i] = sd[(2 * t + 1) * 9 + i]; }
+      merge8(l, r, o);
+    }
+    lvl >>= 1;
+    lbase >>= 1;
+    __syncthreads();
+    if (t < s) {
+#pragma unroll
+      for (int i = 0; i < 8; i++) sd[t * 9 + i] = o[i];
+      store_digest(a.nodes + (lvl + lbase + t) * 8, o);
+    }
   }
 }
 
@@ -623,7 +716,7 @@ __global__ __launch_bounds__(TPB) void k_deep(DeepArgs a, const felt* __restrict
 // fold-by-16: u = iDFT16(row) (unscaled), result = (1/16) sum_k u_k beta^k,
 // beta = alpha / x_r; eps_inv[m] = w_16^-m for m < 8, eps_inv[8] = 1/16
 __global__ __launch_bounds__(TPB) void k_fri_fold16(const felt* __restrict__ E, uint64_t R, felt alpha,
-                                                    felt off_inv, const felt* __restrict__ itw, uint32_t xsh,
+                                                    felt off_inv, const felt* __restrict__ itw_lev,
                                                     const felt* __restrict__ eps_inv, felt* __restrict__ out) {
   uint64_t r = blockIdx.x * (uint64_t)TPB + threadIdx.x;
   if (r >= R) return;
@@ -660,7 +753,7 @@ __global__ __launch_bounds__(TPB) void k_fri_fold16(const felt* __restrict__ E, 
     v[blk] = add(x, y);
     v[blk + 1] = sub(x, y);
   }
-  felt beta = mul(alpha, mul(off_inv, itw[r << xsh]));
+  felt beta = mul(alpha, mul(off_inv, itw_lev[r]));
   // Horner over k = 15..0 with u_k = v[rev4(k)]
   // u_k = v[rev4(k)], rev4 = {0,8,4,12,2,10,6,14,1,9,5,13,3,11,7,15}
   felt acc = v[15];
@@ -866,6 +959,11 @@ void launch_ntt(Prof& prof, hipStream_t s, const NttBatch& b, uint32_t logn, boo
   }
 }
 
+void launch_build_levels(Prof& prof, hipStream_t s, felt* tab, uint32_t top) {
+  LAUNCH(prof, "build_levels", s, (double)(1ull << top) * 32.0,
+         hipLaunchKernelGGL(k_build_levels, dim3(grid_stride_blocks(1ull << top)), dim3(TPB), 0, s, tab, top));
+}
+
 void launch_expand_powers(Prof& prof, hipStream_t s, felt* out, uint64_t count, const felt* lo_tab,
                           const felt* hi_tab) {
   LAUNCH(prof, "expand_powers", s, count * 16.0,
@@ -884,6 +982,47 @@ void launch_build_ginv(Prof& prof, hipStream_t s, felt* Gi, uint32_t logn, const
   LAUNCH(prof, "build_ginv", s, (double)(1ull << logn) * 16.0,
          hipLaunchKernelGGL(k_build_ginv, dim3(grid_stride_blocks(1ull << logn)), dim3(TPB), 0, s, Gi, logn, gilo,
                             gihi));
+}
+
+// fused tree over L leaves: one launch per 9 levels
+static void merkle_fused_upper(Prof& prof, hipStream_t s, uint32_t* nodes, uint64_t L) {
+  while (L > 1) {
+    MerkleArgs a{};
+    a.nodes = nodes;
+    a.L = L;
+    uint64_t blocks = (L + 511) / 512;
+    LAUNCH(prof, "merkle_fused", s, (double)L * 32.0 + (double)L * 32.0,
+           hipLaunchKernelGGL(k_merkle_fused<2>, dim3((uint32_t)blocks), dim3(256), 0, s, a));
+    L = L >= 512 ? L / 512 : 1;
+  }
+}
+
+void launch_merkle_lde(Prof& prof, hipStream_t s, const felt* lde, uint32_t cols, uint32_t logB, uint64_t n,
+                       uint32_t* nodes, uint64_t L) {
+  MerkleArgs a{};
+  a.src = lde;
+  a.n = n;
+  a.cols = cols;
+  a.logB = logB;
+  a.nodes = nodes;
+  a.L = L;
+  uint64_t blocks = (L + 511) / 512;
+  LAUNCH(prof, "merkle_lde", s, (double)L * (cols * 16.0 + 64.0),
+         hipLaunchKernelGGL(k_merkle_fused<0>, dim3((uint32_t)blocks), dim3(256), 0, s, a));
+  if (L > 512) merkle_fused_upper(prof, s, nodes, L / 512);
+}
+
+void launch_merkle_fri(Prof& prof, hipStream_t s, const felt* E, uint64_t R, uint32_t F, uint32_t* nodes) {
+  MerkleArgs a{};
+  a.src = E;
+  a.R = R;
+  a.cols = F;
+  a.nodes = nodes;
+  a.L = R;
+  uint64_t blocks = (R + 511) / 512;
+  LAUNCH(prof, "merkle_fri", s, (double)R * (F * 16.0 + 64.0),
+         hipLaunchKernelGGL(k_merkle_fused<1>, dim3((uint32_t)blocks), dim3(256), 0, s, a));
+  if (R > 512) merkle_fused_upper(prof, s, nodes, R / 512);
 }
 
 void launch_leaf_hash_lde(Prof& prof, hipStream_t s, const felt* lde, uint32_t cols, uint32_t logB, uint64_t n,
@@ -970,9 +1109,10 @@ void launch_deep(Prof& prof, hipStream_t s, const DeepArgs& a, felt* out) {
 void launch_fri_fold(Prof& prof, hipStream_t s, const felt* E, uint64_t R, uint32_t F, felt alpha, felt off_inv,
                      const felt* itw, uint32_t logN, uint32_t logD, const felt* eps_inv, felt* out) {
   (void)F;  // only 16 is compiled (the reference's fri_folding_factor)
-  uint32_t xsh = logN - logD;
+  (void)logN;
+  const felt* lev = itw + ((1ull << (logD - 1)) - 1);  // w_D^-r, r < D/2
   LAUNCH(prof, "fri_fold16", s, (double)R * (16 * 16.0 + 16.0),
-         hipLaunchKernelGGL(k_fri_fold16, dim3(blocks_for(R)), dim3(TPB), 0, s, E, R, alpha, off_inv, itw, xsh,
+         hipLaunchKernelGGL(k_fri_fold16, dim3(blocks_for(R)), dim3(TPB), 0, s, E, R, alpha, off_inv, lev,
                             eps_inv, out));
 }
 

@@ -387,7 +387,9 @@ struct zkp_ctx {
     prof.pending.clear();
   }
 
-  // ---- twiddle tables for domain 2^logN: tw[e] = w^e, itw[e] = w^-e (e < N/2)
+  // ---- stage-major twiddle tables for domain 2^logN: level t (t < logN) holds
+  // w_{2^(t+1)}^(+-j), j < 2^t, at [2^t - 1, 2^(t+1) - 1). Level logN-1 is
+  // w_N^(+-e), e < N/2 (the x-coordinate table of the LDE domain).
   std::map<uint32_t, bool> have_tw;
   void ensure_twiddles(uint32_t logN) {
     if (have_tw[logN]) return;
@@ -405,14 +407,19 @@ struct zkp_ctx {
       felt* dhi = buf<felt>("tmp_hi", hi.size());
       upload(dlo, lo.data(), lo.size() * 16);
       upload(dhi, hi.data(), hi.size() * 16);
-      felt* t = buf<felt>((dir ? "itw_" : "tw_") + std::to_string(logN), half);
-      launch_expand_powers(prof, stream, t, half, dlo, dhi);
+      felt* t = buf<felt>((dir ? "itw_" : "tw_") + std::to_string(logN), 2 * half);
+      launch_expand_powers(prof, stream, t + (half - 1), half, dlo, dhi);
+      if (logN > 1) launch_build_levels(prof, stream, t, logN - 1);
       sync();
     }
     have_tw[logN] = true;
   }
-  felt* tw(uint32_t logN) { return reinterpret_cast<felt*>(bufs["tw_" + std::to_string(logN)].p); }
-  felt* itw(uint32_t logN) { return reinterpret_cast<felt*>(bufs["itw_" + std::to_string(logN)].p); }
+  // stage-major tables (NTT kernels, FRI fold)
+  felt* tws(uint32_t logN) { return reinterpret_cast<felt*>(bufs["tw_" + std::to_string(logN)].p); }
+  felt* itws(uint32_t logN) { return reinterpret_cast<felt*>(bufs["itw_" + std::to_string(logN)].p); }
+  // top level: w_N^e, e < N/2 (x-coordinates)
+  felt* tw(uint32_t logN) { return tws(logN) + ((1ull << (logN - 1)) - 1); }
+  felt* itw(uint32_t logN) { return itws(logN) + ((1ull << (logN - 1)) - 1); }
 
   // ---- coset tables for (n, B): S[j*n + p] = n^-1 (g w_N^j)^rev(p) ; Gi[p] = g^-rev(p)
   std::map<std::pair<uint32_t, uint32_t>, bool> have_coset;
@@ -475,12 +482,11 @@ void lde_commit(zkp_ctx* ctx, const felt* d_in, uint32_t w, uint32_t logn, uint3
   ctx->ensure_coset(logn, logB);
   if (!input_is_coef) {
     NttBatch ib{d_in, coef, nullptr, n, n, 1, 1, w};
-    launch_ntt(ctx->prof, ctx->stream, ib, logn, false, ctx->itw(logN), logN);
+    launch_ntt(ctx->prof, ctx->stream, ib, logn, false, ctx->itws(logN), logN);
   }
   NttBatch lb{coef, lde, ctx->S(logn, logB), n, n, 1u << logB, 1u << logB, w << logB};
-  launch_ntt(ctx->prof, ctx->stream, lb, logn, true, ctx->tw(logN), logN);
-  launch_leaf_hash_lde(ctx->prof, ctx->stream, lde, w, logB, n, nodes, N);
-  launch_merkle_tree(ctx->prof, ctx->stream, nodes, N);
+  launch_ntt(ctx->prof, ctx->stream, lb, logn, true, ctx->tws(logN), logN);
+  launch_merkle_lde(ctx->prof, ctx->stream, lde, w, logB, n, nodes, N);
   ctx->download(root, nodes + 8, 32);
 }
 
@@ -631,7 +637,7 @@ int prove_impl(zkp_ctx* ctx, int air_id, const felt* d_trace, uint32_t w, uint64
   uint32_t* ctree = ctx->buf<uint32_t>("ctree", (size_t)16 * N);
   {
     NttBatch ib{comp, comp, nullptr, M, M, 1, 1, 1};
-    launch_ntt(pf, st, ib, logn + logce, false, ctx->itw(logN), logN);
+    launch_ntt(pf, st, ib, logn + logce, false, ctx->itws(logN), logN);
     std::vector<felt> sc(C);
     felt nm = mul(felt_u64(n), inv(felt_u64(M)));
     felt ginv_n = inv(pow_u64(g, n));
@@ -709,13 +715,12 @@ int prove_impl(zkp_ctx* ctx, int air_id, const felt* d_trace, uint32_t w, uint64
       layer_size[l] = D;
       uint32_t* nodes = ft + 8 * to;
       layer_trees[l] = nodes;
-      launch_leaf_hash_fri(pf, st, layer_evals[l], R, F, nodes);
-      launch_merkle_tree(pf, st, nodes, R);
+      launch_merkle_fri(pf, st, layer_evals[l], R, F, nodes);
       ctx->download(T.fri_roots[l], nodes + 8, 32);
       coin.reseed(T.fri_roots[l]);
       felt alpha = coin.draw();
       felt* nxt = fe + eo;
-      launch_fri_fold(pf, st, layer_evals[l], R, F, alpha, inv(off), ctx->itw(logN), logN, ilog2(D), deps, nxt);
+      launch_fri_fold(pf, st, layer_evals[l], R, F, alpha, inv(off), ctx->itws(logN), logN, ilog2(D), deps, nxt);
       layer_evals[l + 1] = nxt;
       eo += R;
       to += 2 * R;
@@ -1023,8 +1028,7 @@ int zkp_merkle_commit_rows(zkp_ctx* ctx, const zkp_felt* cols, uint32_t w, uint6
     felt* d = ctx->buf<felt>("mrows", (size_t)w * rows);
     ctx->upload(d, cols, (size_t)w * rows * 16);
     uint32_t* tree = ctx->buf<uint32_t>("mtree", (size_t)16 * rows);
-    launch_leaf_hash_lde(ctx->prof, ctx->stream, d, w, 0, rows, tree, rows);
-    launch_merkle_tree(ctx->prof, ctx->stream, tree, rows);
+    launch_merkle_lde(ctx->prof, ctx->stream, d, w, 0, rows, tree, rows);
     ctx->download(root, tree + 8, 32);
     ctx->collect_prof();
     return 0;

@@ -42,12 +42,15 @@ struct NttBatch {
   uint32_t src_div, scale_mod, batches;
 };
 
-// Full transform over `batches` arrays of size 2^logn using twiddle table
-// tw[e] = w_{2^logN}^e (e < 2^logN / 2) of the largest domain (logN >= logn).
+// Full transform over `batches` arrays of size 2^logn using the stage-major
+// twiddle table tw (level t at tw[2^t - 1 .. 2^(t+1) - 1) holds w_{2^(t+1)}^j;
+// forward table for DIT, inverse table for DIF).
 void launch_ntt(Prof& prof, hipStream_t s, const NttBatch& b, uint32_t logn, bool dit, const felt* tw,
                 uint32_t logN);
 
 // ---------------------------------------------------------------- tables
+// fill levels 0..top-1 of a stage-major table whose level `top` is present
+void launch_build_levels(Prof& prof, hipStream_t s, felt* tab, uint32_t top);
 void launch_expand_powers(Prof& prof, hipStream_t s, felt* out, uint64_t count, const felt* lo_tab,
                           const felt* hi_tab);
 // S[j*n + p] = ninv * (g * w_N^j)^rev(p)   (j < B)
@@ -62,6 +65,10 @@ void launch_leaf_hash_lde(Prof& prof, hipStream_t s, const felt* lde, uint32_t c
                           uint64_t n, uint32_t* nodes, uint64_t L);
 // leaves of FRI layer: row r = [E[r + k*R] for k < F] -> nodes[R + r]
 void launch_leaf_hash_fri(Prof& prof, hipStream_t s, const felt* E, uint64_t R, uint32_t F, uint32_t* nodes);
+// fused builders: leaves + all levels (nodes[1..2L)) in ceil(log2(L)/9) launches
+void launch_merkle_lde(Prof& prof, hipStream_t s, const felt* lde, uint32_t cols, uint32_t logB, uint64_t n,
+                       uint32_t* nodes, uint64_t L);
+void launch_merkle_fri(Prof& prof, hipStream_t s, const felt* E, uint64_t R, uint32_t F, uint32_t* nodes);
 // internal nodes nodes[1..L) from leaves nodes[L..2L)
 void launch_merkle_tree(Prof& prof, hipStream_t s, uint32_t* nodes, uint64_t L);
 void launch_grind(Prof& prof, hipStream_t s, const uint32_t* seed_words_dev, uint64_t base, uint64_t count,
