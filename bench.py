@@ -39,6 +39,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--stats", action="store_true", help="print the per-kernel table to stderr")
+    ap.add_argument("--air", choices=["mimc", "agg"], default="mimc",
+                    help="mimc = C2 (default, the BASELINE metric); agg = C3 GlobalUpdate (64 updates, 2^18 rows)")
     return ap.parse_args()
 
 
@@ -60,14 +62,32 @@ def main():
             import torch
             torch.cuda.synchronize()
 
-    from zk_stark_project_amd import AIR_MIMC, MimcProver, ProofOptions
+    from zk_stark_project_amd import AIR_GLOBAL_UPDATE, AIR_MIMC, GlobalUpdateProver, MimcProver, ProofOptions
     from zk_stark_project_amd import _native
+    from zk_stark_project_amd.helper import f64_to_felt
 
-    n = 1 << args.log_n
-    opts = ProofOptions(40, args.blowup, 21)  # (40, 8, 21, None, 16, 7, Algebraic, Algebraic)
     ctx = _native.Context(local_rank)
-    prover = MimcProver(opts, ctx)
-    trace = prover.build_trace(42 * 10**6 + rank, n)  # independent trace per rank
+    if args.air == "mimc":
+        air_id, width = AIR_MIMC, 1
+        n = 1 << args.log_n
+        opts = ProofOptions(40, args.blowup, 21)  # (40, 8, 21, None, 16, 7, Algebraic, Algebraic)
+        prover = MimcProver(opts, ctx)
+        trace = prover.build_trace(42 * 10**6 + rank, n)  # independent trace per rank
+        workload = f"MiMC AIR 2^{args.log_n}-step trace, blowup={args.blowup} (BASELINE configs[1])"
+    else:
+        import random
+        air_id, width = AIR_GLOBAL_UPDATE, 120
+        n = 1 << (18 if args.log_n == 20 else args.log_n)
+        opts = ProofOptions.reference()  # (40, 16, 21, None, 16, 7, Algebraic, Algebraic)
+        rnd = random.Random(1 + rank)
+        r = lambda: rnd.randrange(2**64)
+        ndev = 64
+        prover = GlobalUpdateProver(opts, [[r() for _ in range(9)] for _ in range(6)], [r() for _ in range(6)],
+                                    [[[r() for _ in range(9)] for _ in range(6)] for _ in range(ndev)],
+                                    [[r() for _ in range(6)] for _ in range(ndev)], f64_to_felt(ndev),
+                                    trace_length=n, blinding=[r() for _ in range(60)], ctx=ctx)
+        trace = prover.build_trace()
+        workload = f"GlobalUpdate AIR, {ndev} updates padded to 2^{n.bit_length() - 1} rows, w=120 (BASELINE configs[2])"
     pub = prover.get_pub_inputs(trace).to_elements()
     d_trace = ctx.alloc(trace.data.nbytes)
     ctx.to_device(d_trace, trace.data)
@@ -75,14 +95,14 @@ def main():
     from zk_stark_project_amd.replicas import aggregate_rate, timed_replicas
 
     def prove_once():
-        return ctx.prove_device(AIR_MIMC, d_trace, 1, n, pub, opts)
+        return ctx.prove_device(air_id, d_trace, width, n, pub, opts)
 
     verified = None
     if args.warmup > 0:
         proof, _ = prove_once()
         if rank == 0 and not args.no_verify:
             import oracle_ref  # tests/ checker: the oracle's verifier accepts the GPU proof
-            verified = oracle_ref.verify(AIR_MIMC, proof, b"".join(v.to_bytes(16, "little") for v in pub),
+            verified = oracle_ref.verify(air_id, proof, b"".join(v.to_bytes(16, "little") for v in pub),
                                          opts) == 0
 
     ctx.reset_stats()
@@ -98,6 +118,8 @@ def main():
             dist.destroy_process_group()
         return
 
+    host_stages = {k: v for k, v in stats.items() if k.startswith("host_")}
+    stats = {k: v for k, v in stats.items() if not k.startswith("host_")}  # device kernels only
     total_ms = sum(v["ms"] for v in stats.values())
     dom_name, dom = max(stats.items(), key=lambda kv: kv[1]["ms"])
     dom_avg_ms = dom["ms"] / dom["launches"]
@@ -122,20 +144,23 @@ def main():
         tb = trace.to_bytes()
         pb = b"".join(v.to_bytes(16, "little") for v in pub)
         t1 = time.perf_counter()
-        cproof, _ = oracle_ref.prove(AIR_MIMC, tb, 1, n, pb, opts)
+        cproof, _ = oracle_ref.prove(air_id, tb, width, n, pb, opts)
         dt = time.perf_counter() - t1
         cpu = {
             "value": round(1.0 / dt, 5),
             "unit": "proofs/s",
             "cores": oracle_ref.lib().oracle_num_threads(),
             "kind": "port",
-            "sample": f"one full MiMC 2^{args.log_n} proof (C oracle restating the winterfell 0.12 CPU path, "
-                      f"OpenMP), {dt * 1e3:.0f} ms; proof bytes identical to GPU: {cproof == proof}",
+            "sample": f"one full proof of the same workload ({workload}) by the C oracle restating the "
+                      f"winterfell 0.12 CPU path (OpenMP), {dt * 1e3:.0f} ms; proof bytes identical to GPU: "
+                      f"{cproof == proof}",
         }
 
     ms = elapsed / args.steps * 1e3
+    metric = ("STARK proofs/sec + prove-time ms, MiMC AIR 2^20-step trace" if args.air == "mimc"
+              else "STARK proofs/sec + prove-time ms, aggregation AIR 2^18-step trace (C3)")
     out = {
-        "metric": "STARK proofs/sec + prove-time ms, MiMC AIR 2^20-step trace",
+        "metric": metric,
         "value": round(aggregate_rate(world, args.steps, elapsed), 3),
         "unit": "proofs/s",
         "n_gpus": world,
@@ -146,9 +171,10 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f128 (u128 mod 2^128-45*2^40+1)",
-        "data": "synthetic (MiMC trace x0=42e6+rank)",
-        "config": {"workload": f"MiMC AIR 2^{args.log_n}-step trace, blowup={args.blowup} (BASELINE configs[1])",
-                   "trace_length": n, "blowup": args.blowup, "num_queries": 40, "grinding": 21,
+        "data": "synthetic (MiMC trace x0=42e6+rank)" if args.air == "mimc" else "synthetic (seeded u64 model entries)",
+        "config": {"workload": workload,
+                   "trace_length": n, "trace_width": width, "blowup": opts.blowup_factor, "num_queries": 40,
+                   "grinding": 21,
                    "fri_folding": 16, "fri_remainder_max_degree": 7, "parallelism": f"replicas{world}"},
         "roofline": roofline,
         "cpu_baseline": cpu,
@@ -157,6 +183,8 @@ def main():
     }
     print(json.dumps(out))
     if args.stats:
+        for k, v in sorted(host_stages.items()):
+            print(f"{k:26s} calls={v['launches']:6d} wall_ms={v['ms']:9.3f}", file=sys.stderr)
         for k, v in sorted(stats.items(), key=lambda kv: -kv[1]["ms"]):
             print(f"{k:20s} launches={v['launches']:6d} ms={v['ms']:9.3f} "
                   f"GB/s={v['bytes'] / (v['ms'] * 1e-3) / 1e9 if v['ms'] else 0:9.1f}", file=sys.stderr)

@@ -92,3 +92,46 @@ def test_global_update_proof_bit_exact(ctx, ndev, n):
     assert bytes(gtr.constraint_root) == bytes(otr.constraint_root)
     assert gpu == ref
     assert O.verify(AIR_GLOBAL_UPDATE, gpu, pub, opts) == 0
+
+
+# ---------------------------------------------------------------- full-size configs
+@pytest.mark.slow
+def test_mimc_c2_full_size_bit_exact(ctx):
+    """C2: MiMC 2^20, blowup 8, grinding 21 — GPU bytes == oracle bytes, oracle verifier accepts."""
+    opts = ProofOptions(40, 8, 21)
+    p, trace = mimc_case(1 << 20, opts)
+    pub_el = p.get_pub_inputs(trace).to_elements()
+    gpu, _ = ctx.prove(AIR_MIMC, trace.data, pub_el, opts)
+    ref, _ = O.prove(AIR_MIMC, trace.to_bytes(), 1, 1 << 20, to_bytes(pub_el), opts)
+    assert gpu == ref
+    assert O.verify(AIR_MIMC, gpu, to_bytes(pub_el), opts) == 0
+
+
+@pytest.mark.slow
+def test_global_update_c3_full_size(ctx):
+    """C3: GlobalUpdate AIR, 64 device updates padded to 2^18 rows, reference options
+    (40, 16, 21): GPU proof == oracle proof and verifies."""
+    opts = ProofOptions.reference()
+    p = gu_prover(64, 1 << 18, opts, seed=3)
+    trace = p.build_trace()
+    pub_el = p.get_pub_inputs(trace).to_elements()
+    gpu, gtr = ctx.prove(AIR_GLOBAL_UPDATE, trace.data, pub_el, opts)
+    assert O.verify(AIR_GLOBAL_UPDATE, gpu, to_bytes(pub_el), opts) == 0
+    ref, otr = O.prove(AIR_GLOBAL_UPDATE, trace.to_bytes(), 120, 1 << 18, to_bytes(pub_el), opts)
+    assert bytes(gtr.trace_root) == bytes(otr.trace_root)
+    assert gpu == ref
+
+
+@pytest.mark.slow
+def test_global_update_c5_size_single_gpu(ctx):
+    """C5 trace shape (256 updates, 2^20 rows x 120 cols, 32 GiB LDE) on one GPU:
+    the proof verifies and a mutated public input is rejected (size-independent checks)."""
+    opts = ProofOptions.reference()
+    p = gu_prover(256, 1 << 20, opts, seed=4)
+    trace = p.build_trace()
+    pub_el = p.get_pub_inputs(trace).to_elements()
+    gpu, _ = ctx.prove(AIR_GLOBAL_UPDATE, trace.data, pub_el, opts)
+    assert O.verify(AIR_GLOBAL_UPDATE, gpu, to_bytes(pub_el), opts) == 0
+    bad = list(pub_el)
+    bad[60] = (bad[60] + 1) % P
+    assert O.verify(AIR_GLOBAL_UPDATE, gpu, to_bytes(bad), opts) != 0

@@ -179,56 +179,76 @@ __global__ __launch_bounds__(NT) void k_ntt8(Ntt8Args a) {
   const uint32_t tid = threadIdx.x;
   constexpr uint32_t LOGNT = NT == 1024 ? 10 : (NT == 512 ? 9 : 8);
 
-  // coalesced global -> LDS (element order: ll fastest, then q, then hl)
-#pragma unroll
-  for (int i = 0; i < 8; i++) {
-    uint32_t e = tid + i * NT;
-    uint32_t ll = e & (Tl - 1);
-    uint32_t rest = e >> a.logTl;
-    uint32_t q = rest & qmask;
-    uint32_t hl = rest >> K;
-    uint64_t addr = ((hi0 + hl) << (lo + K)) + ((uint64_t)q << lo) + l0 + ll;
-    felt v = src[addr];
-    if (scale) v = mul(v, scale[addr]);
-    lds[q * TP + (hl * Tl + ll)] = v;
-  }
-
+  // global address of block-local element (gg, q)
+  auto gaddr = [&](uint32_t gg, uint32_t q) -> uint64_t {
+    uint32_t hl = gg >> a.logTl, ll = gg & (Tl - 1);
+    return ((hi0 + hl) << (lo + K)) + ((uint64_t)q << lo) + l0 + ll;
+  };
+  (void)qmask;
   uint32_t b0 = DIT ? 0 : K;
   for (uint32_t r = 0; r < a.nrounds; r++) {
     const uint32_t rb = a.rbits[r];
     if (!DIT) b0 -= rb;
-    __syncthreads();
+    const bool first = r == 0, last = r + 1 == a.nrounds;
+    if (!first) __syncthreads();
     felt x[8];
-    uint32_t idx[8];
     uint32_t ggs[2], qlow[2];
+    // block-local coordinates (gg, q) of register m in this round
+    auto coord_gg = [&](int m) { return ((uint32_t)(m >> rb) << LOGNT | tid) & (T - 1); };
+    auto coord_q = [&](int m) {
+      uint32_t extra = m >> rb, bf = m & ((1u << rb) - 1);
+      uint32_t qo = ((extra << LOGNT) | tid) >> a.logT;
+      uint32_t ql = qo & ((1u << b0) - 1);
+      return ((qo >> b0) << (b0 + rb)) | (bf << b0) | ql;
+    };
 #pragma unroll
     for (int m = 0; m < 8; m++) {
       uint32_t extra = m >> rb, bf = m & ((1u << rb) - 1);
       uint32_t c = (extra << LOGNT) | tid;
-      uint32_t gg = c & (T - 1);
-      uint32_t qo = c >> a.logT;
-      uint32_t ql = qo & ((1u << b0) - 1);
-      uint32_t q = ((qo >> b0) << (b0 + rb)) | (bf << b0) | ql;
-      idx[m] = q * TP + gg;
-      x[m] = lds[idx[m]];
-      if (bf == 0 && extra < 2) { ggs[extra] = gg; qlow[extra] = ql; }
+      if (first) {  // straight from HBM (coalesced along gg), coset scale fused
+        uint64_t ad = gaddr(coord_gg(m), coord_q(m));
+        felt v = src[ad];
+        if (scale) v = mul(v, scale[ad]);
+        x[m] = v;
+      } else {
+        x[m] = lds[coord_q(m) * TP + coord_gg(m)];
+      }
+      if (bf == 0 && extra < 2) { ggs[extra] = c & (T - 1); qlow[extra] = (c >> a.logT) & ((1u << b0) - 1); }
     }
     if (rb == 3) {
       const uint64_t l = l0 + (ggs[0] & (Tl - 1));
       const uint64_t jb = ((uint64_t)qlow[0] << lo) | l;
-      felt w0 = ntt_tw<DIT>(a, jb, b0);
-      felt w1a = ntt_tw<DIT>(a, jb, b0 + 1), w1b = ntt_tw<DIT>(a, jb | (1ull << (b0 + lo)), b0 + 1);
-      felt w2[4];
-#pragma unroll
-      for (int k2 = 0; k2 < 4; k2++) w2[k2] = ntt_tw<DIT>(a, jb | ((uint64_t)k2 << (b0 + lo)), b0 + 2);
+      const uint64_t jstep = 1ull << (b0 + lo);
       if (DIT) {
-        bfly<true>(x[0], x[1], w0); bfly<true>(x[2], x[3], w0); bfly<true>(x[4], x[5], w0); bfly<true>(x[6], x[7], w0);
-        bfly<true>(x[0], x[2], w1a); bfly<true>(x[1], x[3], w1b); bfly<true>(x[4], x[6], w1a); bfly<true>(x[5], x[7], w1b);
-        bfly<true>(x[0], x[4], w2[0]); bfly<true>(x[1], x[5], w2[1]); bfly<true>(x[2], x[6], w2[2]); bfly<true>(x[3], x[7], w2[3]);
+        {
+          felt w0 = ntt_tw<true>(a, jb, b0);
+          bfly<true>(x[0], x[1], w0); bfly<true>(x[2], x[3], w0); bfly<true>(x[4], x[5], w0); bfly<true>(x[6], x[7], w0);
+        }
+        {
+          felt w1a = ntt_tw<true>(a, jb, b0 + 1);
+          bfly<true>(x[0], x[2], w1a); bfly<true>(x[4], x[6], w1a);
+          felt w1b = ntt_tw<true>(a, jb | jstep, b0 + 1);
+          bfly<true>(x[1], x[3], w1b); bfly<true>(x[5], x[7], w1b);
+        }
+        static_for<0, 4>([&](auto k2) {
+          felt w2 = ntt_tw<true>(a, jb | ((uint64_t)k2 << (b0 + lo)), b0 + 2);
+          bfly<true>(x[k2], x[k2 + 4], w2);
+        });
       } else {
-        bfly<false>(x[0], x[4], w2[0]); bfly<false>(x[1], x[5], w2[1]); bfly<false>(x[2], x[6], w2[2]); bfly<false>(x[3], x[7], w2[3]);
-        bfly<false>(x[0], x[2], w1a); bfly<false>(x[1], x[3], w1b); bfly<false>(x[4], x[6], w1a); bfly<false>(x[5], x[7], w1b);
-        bfly<false>(x[0], x[1], w0); bfly<false>(x[2], x[3], w0); bfly<false>(x[4], x[5], w0); bfly<false>(x[6], x[7], w0);
+        static_for<0, 4>([&](auto k2) {
+          felt w2 = ntt_tw<false>(a, jb | ((uint64_t)k2 << (b0 + lo)), b0 + 2);
+          bfly<false>(x[k2], x[k2 + 4], w2);
+        });
+        {
+          felt w1a = ntt_tw<false>(a, jb, b0 + 1);
+          bfly<false>(x[0], x[2], w1a); bfly<false>(x[4], x[6], w1a);
+          felt w1b = ntt_tw<false>(a, jb | jstep, b0 + 1);
+          bfly<false>(x[1], x[3], w1b); bfly<false>(x[5], x[7], w1b);
+        }
+        {
+          felt w0 = ntt_tw<false>(a, jb, b0);
+          bfly<false>(x[0], x[1], w0); bfly<false>(x[2], x[3], w0); bfly<false>(x[4], x[5], w0); bfly<false>(x[6], x[7], w0);
+        }
       }
     } else if (rb == 2) {
 #pragma unroll
@@ -256,20 +276,13 @@ __global__ __launch_bounds__(NT) void k_ntt8(Ntt8Args a) {
         bfly<DIT>(x[2 * u], x[2 * u + 1], ntt_tw<DIT>(a, jb, b0));
       }
     }
+    if (!last) __syncthreads();  // everyone has read this round's slots
 #pragma unroll
-    for (int m = 0; m < 8; m++) lds[idx[m]] = x[m];
+    for (int m = 0; m < 8; m++) {
+      if (last) dst[gaddr(coord_gg(m), coord_q(m))] = x[m];  // straight to HBM
+      else lds[coord_q(m) * TP + coord_gg(m)] = x[m];
+    }
     if (DIT) b0 += rb;
-  }
-  __syncthreads();
-#pragma unroll
-  for (int i = 0; i < 8; i++) {
-    uint32_t e = tid + i * NT;
-    uint32_t ll = e & (Tl - 1);
-    uint32_t rest = e >> a.logTl;
-    uint32_t q = rest & qmask;
-    uint32_t hl = rest >> K;
-    uint64_t addr = ((hi0 + hl) << (lo + K)) + ((uint64_t)q << lo) + l0 + ll;
-    dst[addr] = lds[q * TP + (hl * Tl + ll)];
   }
   (void)E;
 }
@@ -443,6 +456,32 @@ __global__ __launch_bounds__(256) void k_merkle_fused(MerkleArgs a) {
       store_digest(a.nodes + (lvl + lbase + t) * 8, o);
     }
   }
+}
+
+// Lane-subtree Merkle build: every lane turns 2^H consecutive leaves into their
+// height-H subtree sequentially in registers (compile-time recursion, <= H+1
+// live digests), writing every node it creates. No LDS, no barriers, no idle
+// lanes; the levels above are built by further passes over the subtree roots.
+template <int MODE, int H>
+__device__ __forceinline__ void lane_subtree(const MerkleArgs& a, uint64_t base, uint32_t out[8]) {
+  if constexpr (H == 0) {
+    merkle_leaf<MODE>(a, base, out);
+    if (MODE != 2) store_digest(a.nodes + (a.L + base) * 8, out);
+  } else {
+    uint32_t l[8], r[8];
+    lane_subtree<MODE, H - 1>(a, base, l);
+    lane_subtree<MODE, H - 1>(a, base + (1ull << (H - 1)), r);
+    merge8(l, r, out);
+    store_digest(a.nodes + ((a.L >> H) + (base >> H)) * 8, out);
+  }
+}
+
+template <int MODE, int H>
+__global__ __launch_bounds__(256) void k_merkle_lane(MerkleArgs a) {
+  const uint64_t lane = blockIdx.x * (uint64_t)256 + threadIdx.x;
+  if (lane >= (a.L >> H)) return;
+  uint32_t root[8];
+  lane_subtree<MODE, H>(a, lane << H, root);
 }
 
 struct SeedArg {
@@ -775,6 +814,19 @@ __global__ __launch_bounds__(TPB) void k_fri_fold16(const felt* __restrict__ E, 
   out[r] = mul(acc, eps_inv[8]);
 }
 
+// multi-segment gather: segment s copies seg[s].count items of seg[s].words
+// 32-bit words from src (item index idx[seg.idx_off + i]) to out + seg.out_off
+__global__ void k_gather_multi(const GatherSeg* __restrict__ segs, const uint64_t* __restrict__ idx,
+                               uint32_t* __restrict__ out) {
+  const GatherSeg sg = segs[blockIdx.y];
+  uint64_t i = blockIdx.x * (uint64_t)TPB + threadIdx.x;
+  if (i >= sg.count) return;
+  const uint32_t* src = reinterpret_cast<const uint32_t*>(sg.src) + idx[sg.idx_off + i] * sg.words;
+  uint32_t* dst = out + sg.out_off + i * sg.words;
+  for (uint32_t w = 0; w < sg.words; w += 4)
+    *reinterpret_cast<uint4*>(dst + w) = *reinterpret_cast<const uint4*>(src + w);
+}
+
 __global__ void k_gather_felts(const felt* __restrict__ src, const uint64_t* __restrict__ idx, felt* __restrict__ out,
                                uint64_t count) {
   uint64_t i = blockIdx.x * (uint64_t)TPB + threadIdx.x;
@@ -984,16 +1036,36 @@ void launch_build_ginv(Prof& prof, hipStream_t s, felt* Gi, uint32_t logn, const
                             gihi));
 }
 
-// fused tree over L leaves: one launch per 9 levels
-static void merkle_fused_upper(Prof& prof, hipStream_t s, uint32_t* nodes, uint64_t L) {
+// tree build by lane-subtree passes: pass 1 hashes leaves and builds H0 levels,
+// later passes build up to 4 levels each from the stored subtree roots.
+template <int MODE>
+static void merkle_pass(Prof& prof, hipStream_t s, const MerkleArgs& a, uint32_t H, const char* name, double bytes) {
+  uint64_t lanes = a.L >> H;
+  dim3 g(blocks_for(lanes));
+  switch (H) {
+    case 1: LAUNCH(prof, name, s, bytes, hipLaunchKernelGGL((k_merkle_lane<MODE, 1>), g, dim3(256), 0, s, a)); break;
+    case 2: LAUNCH(prof, name, s, bytes, hipLaunchKernelGGL((k_merkle_lane<MODE, 2>), g, dim3(256), 0, s, a)); break;
+    case 3: LAUNCH(prof, name, s, bytes, hipLaunchKernelGGL((k_merkle_lane<MODE, 3>), g, dim3(256), 0, s, a)); break;
+    default: LAUNCH(prof, name, s, bytes, hipLaunchKernelGGL((k_merkle_lane<MODE, 4>), g, dim3(256), 0, s, a)); break;
+  }
+}
+
+// upper levels: wide levels by lane passes (4 levels each), the narrow top by
+// the LDS-fused kernel (9 levels per launch, parallel tail)
+static void merkle_upper(Prof& prof, hipStream_t s, uint32_t* nodes, uint64_t L) {
   while (L > 1) {
     MerkleArgs a{};
     a.nodes = nodes;
     a.L = L;
-    uint64_t blocks = (L + 511) / 512;
-    LAUNCH(prof, "merkle_fused", s, (double)L * 32.0 + (double)L * 32.0,
-           hipLaunchKernelGGL(k_merkle_fused<2>, dim3((uint32_t)blocks), dim3(256), 0, s, a));
-    L = L >= 512 ? L / 512 : 1;
+    if (L >= (1ull << 13)) {
+      merkle_pass<2>(prof, s, a, 4, "merkle_upper", (double)L * 32.0 * 1.5);
+      L >>= 4;
+    } else {
+      uint64_t blocks = (L + 511) / 512;
+      LAUNCH(prof, "merkle_top9", s, (double)L * 64.0,
+             hipLaunchKernelGGL(k_merkle_fused<2>, dim3((uint32_t)blocks), dim3(256), 0, s, a));
+      L = L >= 512 ? L / 512 : 1;
+    }
   }
 }
 
@@ -1006,10 +1078,10 @@ void launch_merkle_lde(Prof& prof, hipStream_t s, const felt* lde, uint32_t cols
   a.logB = logB;
   a.nodes = nodes;
   a.L = L;
-  uint64_t blocks = (L + 511) / 512;
-  LAUNCH(prof, "merkle_lde", s, (double)L * (cols * 16.0 + 64.0),
-         hipLaunchKernelGGL(k_merkle_fused<0>, dim3((uint32_t)blocks), dim3(256), 0, s, a));
-  if (L > 512) merkle_fused_upper(prof, s, nodes, L / 512);
+  uint32_t H = 0;
+  while (H < 3 && (1ull << (H + 1)) <= L) H++;
+  merkle_pass<0>(prof, s, a, H, "merkle_lde", (double)L * (cols * 16.0 + 64.0));
+  merkle_upper(prof, s, nodes, L >> H);
 }
 
 void launch_merkle_fri(Prof& prof, hipStream_t s, const felt* E, uint64_t R, uint32_t F, uint32_t* nodes) {
@@ -1019,10 +1091,10 @@ void launch_merkle_fri(Prof& prof, hipStream_t s, const felt* E, uint64_t R, uin
   a.cols = F;
   a.nodes = nodes;
   a.L = R;
-  uint64_t blocks = (R + 511) / 512;
-  LAUNCH(prof, "merkle_fri", s, (double)R * (F * 16.0 + 64.0),
-         hipLaunchKernelGGL(k_merkle_fused<1>, dim3((uint32_t)blocks), dim3(256), 0, s, a));
-  if (R > 512) merkle_fused_upper(prof, s, nodes, R / 512);
+  uint32_t H = 0;
+  while (H < 2 && (1ull << (H + 1)) <= R) H++;
+  merkle_pass<1>(prof, s, a, H, "merkle_fri", (double)R * (F * 16.0 + 64.0));
+  merkle_upper(prof, s, nodes, R >> H);
 }
 
 void launch_leaf_hash_lde(Prof& prof, hipStream_t s, const felt* lde, uint32_t cols, uint32_t logB, uint64_t n,
@@ -1114,6 +1186,12 @@ void launch_fri_fold(Prof& prof, hipStream_t s, const felt* E, uint64_t R, uint3
   LAUNCH(prof, "fri_fold16", s, (double)R * (16 * 16.0 + 16.0),
          hipLaunchKernelGGL(k_fri_fold16, dim3(blocks_for(R)), dim3(TPB), 0, s, E, R, alpha, off_inv, lev,
                             eps_inv, out));
+}
+
+void launch_gather_multi(Prof& prof, hipStream_t s, const GatherSeg* segs, uint32_t nseg, uint64_t max_count,
+                         const uint64_t* idx, uint32_t* out, double bytes) {
+  LAUNCH(prof, "gather", s, bytes,
+         hipLaunchKernelGGL(k_gather_multi, dim3(blocks_for(max_count), nseg), dim3(TPB), 0, s, segs, idx, out));
 }
 
 void launch_gather_felts(Prof& prof, hipStream_t s, const felt* src, const uint64_t* idx, felt* out, uint64_t count) {

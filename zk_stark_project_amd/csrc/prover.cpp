@@ -8,6 +8,7 @@
 // GPU (kernels.hip); the host only drives the Fiat-Shamir transcript and
 // assembles the proof bytes from the few values the verifier needs.
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -342,6 +343,19 @@ struct zkp_ctx {
   };
   std::map<std::string, Stat> stats;
   std::vector<void*> user_allocs;
+  // pinned host staging (fast small H2D/D2H transfers)
+  void* pinned_p = nullptr;
+  size_t pinned_bytes = 0;
+  void* pinned(size_t bytes) {
+    if (pinned_bytes < bytes) {
+      if (pinned_p) HIP_CHECK(hipHostFree(pinned_p));
+      pinned_p = nullptr;
+      size_t nb = bytes < (1u << 20) ? (1u << 20) : bytes;
+      HIP_CHECK(hipHostMalloc(&pinned_p, nb, hipHostMallocDefault));
+      pinned_bytes = nb;
+    }
+    return pinned_p;
+  }
 
   template <typename T>
   T* buf(const std::string& name, size_t count) {
@@ -364,12 +378,50 @@ struct zkp_ctx {
     cached[key] = true;
     return had;
   }
+  // small uploads are staged in a pinned ring that is only reset between proofs
+  // (the stream is in order, so a slot is never overwritten while in flight)
+  uint8_t* ring_p = nullptr;
+  size_t ring_cap = 0, ring_off = 0;
+  void ring_reset() { ring_off = 0; }
   void upload(void* d, const void* h, size_t bytes) {
-    HIP_CHECK(hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, stream));
+    if (bytes > (1u << 20)) {
+      HIP_CHECK(hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, stream));
+      return;
+    }
+    if (!ring_p) {
+      ring_cap = 8u << 20;
+      HIP_CHECK(hipHostMalloc((void**)&ring_p, ring_cap, hipHostMallocDefault));
+    }
+    size_t need = (bytes + 255) & ~(size_t)255;
+    if (ring_off + need > ring_cap) {  // wrap: wait until earlier copies are done
+      sync();
+      ring_off = 0;
+    }
+    memcpy(ring_p + ring_off, h, bytes);
+    HIP_CHECK(hipMemcpyAsync(d, ring_p + ring_off, bytes, hipMemcpyHostToDevice, stream));
+    ring_off += need;
   }
   void download(void* h, const void* d, size_t bytes) {
-    HIP_CHECK(hipMemcpyAsync(h, d, bytes, hipMemcpyDeviceToHost, stream));
+    if (bytes > (1u << 20)) {
+      HIP_CHECK(hipMemcpyAsync(h, d, bytes, hipMemcpyDeviceToHost, stream));
+      sync();
+      return;
+    }
+    void* hp = pinned(bytes);
+    HIP_CHECK(hipMemcpyAsync(hp, d, bytes, hipMemcpyDeviceToHost, stream));
     sync();
+    memcpy(h, hp, bytes);
+  }
+  // host-side stage clock (profiling only): adds wall ms per stage as "host_<stage>"
+  std::chrono::steady_clock::time_point stage_t0;
+  void stage_begin() { if (prof.enabled) stage_t0 = std::chrono::steady_clock::now(); }
+  void stage_end(const char* name) {
+    if (!prof.enabled) return;
+    auto t = std::chrono::steady_clock::now();
+    auto& s = stats[std::string("host_") + name];
+    s.launches += 1;
+    s.ms += std::chrono::duration<double, std::milli>(t - stage_t0).count();
+    stage_t0 = t;
   }
   void collect_prof() {
     if (prof.pending.empty()) return;
@@ -465,6 +517,8 @@ struct zkp_ctx {
     for (auto& kv : bufs)
       if (kv.second.p) (void)hipFree(kv.second.p);
     for (void* p : user_allocs) (void)hipFree(p);
+    if (pinned_p) (void)hipHostFree(pinned_p);
+    if (ring_p) (void)hipHostFree(ring_p);
     for (auto e : prof.pool) (void)hipEventDestroy(e);
     if (stream) (void)hipStreamDestroy(stream);
   }
@@ -551,6 +605,9 @@ int prove_impl(zkp_ctx* ctx, int air_id, const felt* d_trace, uint32_t w, uint64
   hipStream_t st = ctx->stream;
   Prof& pf = ctx->prof;
 
+  ctx->sync();
+  ctx->ring_reset();
+  ctx->stage_begin();
   // 1. channel: Context::to_elements || pub_inputs.to_elements
   Coin coin;
   {
@@ -566,6 +623,7 @@ int prove_impl(zkp_ctx* ctx, int air_id, const felt* d_trace, uint32_t w, uint64
   uint32_t* ttree = ctx->buf<uint32_t>("ttree", (size_t)16 * N);
   lde_commit(ctx, d_trace, w, logn, logB, coef, tlde, ttree, false, T.trace_root);
   coin.reseed(T.trace_root);
+  ctx->stage_end("1_trace_commit");
 
   // 3. constraint composition coefficients + evaluation (DefaultConstraintEvaluator)
   const uint32_t ncoef = air.num_t + (uint32_t)air.a_col.size();
@@ -649,6 +707,7 @@ int prove_impl(zkp_ctx* ctx, int air_id, const felt* d_trace, uint32_t w, uint64
     lde_commit(ctx, nullptr, C, logn, logB, acoef, clde, ctree, true, T.constraint_root);
   }
   coin.reseed(T.constraint_root);
+  ctx->stage_end("2_constraints_commit");
 
   // 5. OOD frame
   felt z = coin.draw();
@@ -664,6 +723,7 @@ int prove_impl(zkp_ctx* ctx, int air_id, const felt* d_trace, uint32_t w, uint64
   coin.reseed(dg);
   hash_elements(ood_comp.data(), ood_comp.size(), dg);
   coin.reseed(dg);
+  ctx->stage_end("3_ood");
 
   // 6. DEEP composition evaluations over the LDE domain
   std::vector<felt> gam = draw_coeffs(coin, o->batching_deep, w + C);
@@ -682,6 +742,7 @@ int prove_impl(zkp_ctx* ctx, int air_id, const felt* d_trace, uint32_t w, uint64
     da.binv = ctx->buf<felt>("binv", N / 2048 + 1);
     launch_deep(pf, st, da, deep);
   }
+  ctx->stage_end("4_deep_launch");
 
   // 7. FRI layers (FriProver::build_layers), folding factor 16
   uint32_t L = 0;
@@ -737,6 +798,7 @@ int prove_impl(zkp_ctx* ctx, int air_id, const felt* d_trace, uint32_t w, uint64
     coin.reseed(T.remainder_commitment);
     T.num_fri_layers = L;
   }
+  ctx->stage_end("5_fri");
 
   // 8. grinding: minimum nonce >= 1
   uint64_t nonce = 0;
@@ -760,6 +822,7 @@ int prove_impl(zkp_ctx* ctx, int air_id, const felt* d_trace, uint32_t w, uint64
     }
   }
   T.pow_nonce = nonce;
+  ctx->stage_end("6_grind");
 
   // 9. query positions
   std::vector<uint64_t> pos = coin.draw_integers(o->num_queries, N, nonce);
@@ -792,27 +855,66 @@ int prove_impl(zkp_ctx* ctx, int air_id, const felt* d_trace, uint32_t w, uint64
       cur = fpos[l];
     }
   }
-  auto gather_f = [&](const felt* src, const std::vector<uint64_t>& idx) {
-    std::vector<felt> out(idx.size());
-    if (idx.empty()) return out;
-    uint64_t* di = ctx->buf<uint64_t>("gidx", idx.size());
-    felt* dout = ctx->buf<felt>("gout", idx.size());
-    ctx->upload(di, idx.data(), idx.size() * 8);
-    launch_gather_felts(pf, st, src, di, dout, idx.size());
-    ctx->download(out.data(), dout, out.size() * 16);
-    return out;
-  };
-  auto gather_d = [&](const uint32_t* nodes, const BatchPlan& bp) {
+  // one batched gather for every opened value and Merkle path node
+  struct SegPlan {
+    const void* src;
     std::vector<uint64_t> idx;
-    for (auto& p : bp.paths) idx.insert(idx.end(), p.begin(), p.end());
-    std::vector<uint32_t> out(idx.size() * 8);
-    if (idx.empty()) return out;
-    uint64_t* di = ctx->buf<uint64_t>("gidx", idx.size());
-    uint32_t* dout = ctx->buf<uint32_t>("gdout", idx.size() * 8);
-    ctx->upload(di, idx.data(), idx.size() * 8);
-    launch_gather_digests(pf, st, nodes, di, dout, idx.size());
-    ctx->download(out.data(), dout, out.size() * 4);
-    return out;
+    uint32_t words;
+  };
+  std::vector<SegPlan> plan;
+  auto path_idx = [](const BatchPlan& bp) {
+    std::vector<uint64_t> idx;
+    for (auto& pth : bp.paths) idx.insert(idx.end(), pth.begin(), pth.end());
+    return idx;
+  };
+  plan.push_back({tlde, fidx_t, 4});
+  plan.push_back({ttree, path_idx(bt), 8});
+  plan.push_back({clde, fidx_c, 4});
+  plan.push_back({ctree, path_idx(bc), 8});
+  for (uint32_t l = 0; l < L; l++) {
+    plan.push_back({layer_evals[l], fidx[l], 4});
+    plan.push_back({layer_trees[l], path_idx(bf[l]), 8});
+  }
+  std::vector<GatherSeg> segs;
+  std::vector<uint64_t> all_idx;
+  uint64_t out_words = 0, max_count = 1;
+  for (auto& sp : plan) {
+    GatherSeg g;
+    g.src = sp.src;
+    g.idx_off = all_idx.size();
+    g.count = sp.idx.size();
+    g.out_off = out_words;
+    g.words = sp.words;
+    g.pad = 0;
+    all_idx.insert(all_idx.end(), sp.idx.begin(), sp.idx.end());
+    out_words += g.count * sp.words;
+    max_count = std::max<uint64_t>(max_count, g.count);
+    segs.push_back(g);
+  }
+  size_t seg_bytes = segs.size() * sizeof(GatherSeg), idx_bytes = all_idx.size() * 8;
+  size_t up_bytes = seg_bytes + idx_bytes, down_bytes = out_words * 4;
+  uint8_t* hp = (uint8_t*)ctx->pinned(std::max(up_bytes, down_bytes) + 64);
+  memcpy(hp, segs.data(), seg_bytes);
+  memcpy(hp + seg_bytes, all_idx.data(), idx_bytes);
+  uint8_t* dup = ctx->buf<uint8_t>("gather_in", up_bytes + 16);
+  uint32_t* dout = ctx->buf<uint32_t>("gather_out", out_words + 4);
+  HIP_CHECK(hipMemcpyAsync(dup, hp, up_bytes, hipMemcpyHostToDevice, st));
+  launch_gather_multi(pf, st, (const GatherSeg*)dup, (uint32_t)segs.size(), max_count,
+                      (const uint64_t*)(dup + seg_bytes), dout, (double)down_bytes * 2);
+  HIP_CHECK(hipMemcpyAsync(hp, dout, down_bytes, hipMemcpyDeviceToHost, st));
+  ctx->sync();
+  std::vector<uint32_t> gathered(out_words);
+  memcpy(gathered.data(), hp, down_bytes);
+  size_t seg_cursor = 0;
+  auto next_vals = [&]() {
+    const GatherSeg& g = segs[seg_cursor++];
+    std::vector<felt> v(g.count);
+    memcpy(v.data(), gathered.data() + g.out_off, g.count * 16);
+    return v;
+  };
+  auto next_digests = [&]() {
+    const GatherSeg& g = segs[seg_cursor++];
+    return std::vector<uint32_t>(gathered.begin() + g.out_off, gathered.begin() + g.out_off + g.count * 8);
   };
   auto write_batch = [&](Writer& wr, const BatchPlan& bp, const std::vector<uint32_t>& d) {
     wr.u8((uint8_t)bp.depth);
@@ -835,8 +937,8 @@ int prove_impl(zkp_ctx* ctx, int air_id, const felt* d_trace, uint32_t w, uint64
   wr.put(T.remainder_commitment, 32);
   wr.u8(1);
   for (int seg = 0; seg < 2; seg++) {
-    std::vector<felt> vals = gather_f(seg == 0 ? tlde : clde, seg == 0 ? fidx_t : fidx_c);
-    std::vector<uint32_t> dig = gather_d(seg == 0 ? ttree : ctree, seg == 0 ? bt : bc);
+    std::vector<felt> vals = next_vals();
+    std::vector<uint32_t> dig = next_digests();
     Writer vw, pw;
     for (felt v : vals) vw.fe(v);
     write_batch(pw, seg == 0 ? bt : bc, dig);
@@ -850,8 +952,8 @@ int prove_impl(zkp_ctx* ctx, int air_id, const felt* d_trace, uint32_t w, uint64
   for (felt v : ood_comp) wr.fe(v);
   wr.u8((uint8_t)L);
   for (uint32_t l = 0; l < L; l++) {
-    std::vector<felt> vals = gather_f(layer_evals[l], fidx[l]);
-    std::vector<uint32_t> dig = gather_d(layer_trees[l], bf[l]);
+    std::vector<felt> vals = next_vals();
+    std::vector<uint32_t> dig = next_digests();
     Writer vw, pw;
     for (felt v : vals) vw.fe(v);
     write_batch(pw, bf[l], dig);
@@ -864,6 +966,7 @@ int prove_impl(zkp_ctx* ctx, int air_id, const felt* d_trace, uint32_t w, uint64
   wr.u64(nonce);
   wr.u8(0);
 
+  ctx->stage_end("7_queries_serialize");
   ctx->collect_prof();
   uint8_t* out = (uint8_t*)malloc(wr.b.size());
   if (!out) return ZKP_ERR_OOM;

@@ -128,6 +128,14 @@ void launch_fri_fold(Prof& prof, hipStream_t s, const felt* E, uint64_t R, uint3
                      const felt* itw, uint32_t logN, uint32_t logD, const felt* eps_inv_dev, felt* out);
 
 // gathers for query openings
+struct GatherSeg {
+  const void* src;
+  uint64_t idx_off, count, out_off;  // out_off in 32-bit words
+  uint32_t words;                    // 4 (felt) or 8 (digest)
+  uint32_t pad;
+};
+void launch_gather_multi(Prof& prof, hipStream_t s, const GatherSeg* segs, uint32_t nseg, uint64_t max_count,
+                         const uint64_t* idx, uint32_t* out, double bytes);
 void launch_gather_felts(Prof& prof, hipStream_t s, const felt* src, const uint64_t* idx, felt* out, uint64_t count);
 void launch_gather_digests(Prof& prof, hipStream_t s, const uint32_t* nodes, const uint64_t* idx, uint32_t* out,
                            uint64_t count);
