@@ -126,6 +126,33 @@ int zkp_prove_device(zkp_ctx* ctx, zkp_air_id air, const void* d_trace_cols, uin
                      const zkp_proof_options* opts, uint8_t** proof, uint64_t* proof_len,
                      zkp_transcript* transcript /* nullable */);
 
+/* ---- multi-GPU: coset-sharded proving ----
+ * One proof is split over `world` ranks by LDE coset (rank r owns the cosets
+ * [r*B/world, (r+1)*B/world)); the exchange steps are leaf-digest all-to-alls
+ * for the Merkle commitments, an all-to-all + all-gather that reassemble the
+ * composition polynomial, and all-gathers of subtree roots, small FRI layers
+ * and query openings. Every rank passes the full trace and returns the same
+ * proof bytes (identical to zkp_prove's). world must be a power of two <= the
+ * blowup factor; n >= 256 * world.
+ * Replaces, for a multi-GPU node, the single `Prover::prove` call
+ * (src/main.rs:424,468) — the reference itself has no multi-device path. */
+typedef struct zkp_comm zkp_comm;
+/* RCCL communicator (one process per GPU): rank 0 makes the id, the caller
+ * broadcasts its 128 bytes (e.g. with torch.distributed), every rank creates. */
+int zkp_comm_rccl_unique_id(uint8_t id[128]);
+int zkp_comm_rccl_create(zkp_ctx* ctx, const uint8_t id[128], int world, int rank, zkp_comm** out);
+/* In-process group: `world` communicators for ranks run as threads of one
+ * process (each with its own zkp_ctx; GPUs may be shared). comms[world]. */
+int zkp_comm_local_group(int world, zkp_comm** comms);
+void zkp_comm_destroy(zkp_comm* comm);
+int zkp_comm_rank(const zkp_comm* comm);
+int zkp_comm_world(const zkp_comm* comm);
+/* Collective: every rank of `comm` must call it with the same arguments. */
+int zkp_prove_sharded(zkp_ctx* ctx, zkp_comm* comm, zkp_air_id air, const zkp_felt* trace_cols,
+                      uint32_t width, uint64_t n, const zkp_felt* pub_elems, uint64_t n_pub,
+                      const zkp_proof_options* opts, uint8_t** proof, uint64_t* proof_len,
+                      zkp_transcript* transcript /* nullable */);
+
 /* Device scratch helpers so callers (bench, tests) can keep traces in HBM. */
 int zkp_device_alloc(zkp_ctx* ctx, uint64_t bytes, void** d_ptr);
 int zkp_device_free(zkp_ctx* ctx, void* d_ptr);

@@ -1,0 +1,23 @@
+#!/bin/bash
+# Round profile for the judged bench line (run on the GPU box, from the repo root):
+#   1. rocprofv3 --kernel-trace --stats        -> per-kernel average duration
+#   2. rocprofv3 --pmc FETCH_SIZE (own pass)    -> HBM read bytes per dispatch
+#   3. rocprofv3 --pmc WRITE_SIZE (own pass)    -> HBM write bytes per dispatch
+# then scripts/pmc_traffic.py folds them into gpurun_out/prof_<tag>/traffic.json.
+# Usage: scripts/profile_round.sh <tag> [bench args...]
+set -u
+export TMPDIR=/tmp
+TAG=${1:-r01}
+shift || true
+ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
+OUT=$ROOT/gpurun_out/prof_$TAG
+mkdir -p $OUT
+ARGS="--steps 5 --warmup 2 --no-cpu-baseline --no-verify $*"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- \
+  python3 $ROOT/bench.py $ARGS > $OUT/trace.log 2>&1 || { echo "kernel-trace pass failed"; exit 1; }
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -o run -- \
+  python3 $ROOT/bench.py $ARGS > $OUT/fetch.log 2>&1 || { echo "FETCH_SIZE pass failed"; exit 1; }
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -o run -- \
+  python3 $ROOT/bench.py $ARGS > $OUT/write.log 2>&1 || { echo "WRITE_SIZE pass failed"; exit 1; }
+python3 $ROOT/scripts/pmc_traffic.py $OUT > $OUT/traffic.txt || { echo "post-processing failed"; exit 1; }
+echo done

@@ -69,7 +69,8 @@ EXPORTED = [
     "zkp_prove_device", "zkp_device_alloc", "zkp_device_free", "zkp_copy_to_device",
     "zkp_copy_to_host", "zkp_trace_lde_commit", "zkp_merkle_commit_rows", "zkp_grind",
     "zkp_set_profiling", "zkp_kernel_stats", "zkp_reset_stats", "zkp_kernel_stats_table",
-    "zkp_build_mimc_trace",
+    "zkp_build_mimc_trace", "zkp_prove_sharded", "zkp_comm_local_group", "zkp_comm_rccl_unique_id",
+    "zkp_comm_rccl_create", "zkp_comm_destroy", "zkp_comm_rank", "zkp_comm_world",
 ]
 
 _lib = None
@@ -114,6 +115,15 @@ def load():
         L.zkp_kernel_stats_table.argtypes = [vp, ctypes.POINTER(ctypes.c_char_p)]
         L.zkp_build_mimc_trace.argtypes = [ctypes.c_char_p, u64, vp]
         L.zkp_build_mimc_trace.restype = i32
+        L.zkp_prove_sharded.argtypes = [vp, vp, i32, vp, u32, u64, vp, u64, popt, ctypes.POINTER(pu8),
+                                        ctypes.POINTER(u64), ctypes.POINTER(Transcript)]
+        L.zkp_comm_local_group.argtypes = [i32, ctypes.POINTER(vp)]
+        L.zkp_comm_rccl_unique_id.argtypes = [ctypes.c_char_p]
+        L.zkp_comm_rccl_create.argtypes = [vp, ctypes.c_char_p, i32, i32, ctypes.POINTER(vp)]
+        L.zkp_comm_destroy.argtypes = [vp]
+        L.zkp_comm_destroy.restype = None
+        L.zkp_comm_rank.argtypes = [vp]
+        L.zkp_comm_world.argtypes = [vp]
         _lib = L
         return L
 
@@ -126,6 +136,52 @@ def mimc_trace(seed: int, n: int) -> np.ndarray:
     if rc:
         raise ZkpError(rc, "zkp_build_mimc_trace")
     return out
+
+
+class Comm:
+    """Owns one `zkp_comm` (one rank of a coset-sharded proof group)."""
+
+    def __init__(self, ptr: int):
+        self.lib = load()
+        self.ptr = ctypes.c_void_p(ptr)
+
+    @property
+    def rank(self) -> int:
+        return int(self.lib.zkp_comm_rank(self.ptr))
+
+    @property
+    def world(self) -> int:
+        return int(self.lib.zkp_comm_world(self.ptr))
+
+    def close(self):
+        if self.ptr:
+            self.lib.zkp_comm_destroy(self.ptr)
+            self.ptr = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def local_group(world: int) -> list:
+    """`world` communicators of one in-process group (ranks run as threads)."""
+    L = load()
+    arr = (ctypes.c_void_p * world)()
+    rc = L.zkp_comm_local_group(world, arr)
+    if rc:
+        raise ZkpError(rc, "zkp_comm_local_group")
+    return [Comm(arr[i]) for i in range(world)]
+
+
+def rccl_unique_id() -> bytes:
+    L = load()
+    buf = ctypes.create_string_buffer(128)
+    rc = L.zkp_comm_rccl_unique_id(buf)
+    if rc:
+        raise ZkpError(rc, "zkp_comm_rccl_unique_id")
+    return buf.raw
 
 
 class Context:
@@ -182,6 +238,28 @@ class Context:
         data = ctypes.string_at(out, olen.value)
         self.lib.zkp_free(out)
         return data, tr
+
+    def prove_sharded(self, comm: "Comm", air_id: int, trace: np.ndarray, pub, options: ProofOptions):
+        """One rank of a coset-sharded proof (collective over `comm`)."""
+        w, n = int(trace.shape[0]), int(trace.shape[1])
+        pubb = b"".join(int(v).to_bytes(16, "little") for v in pub)
+        out = ctypes.POINTER(ctypes.c_uint8)()
+        olen = ctypes.c_uint64()
+        tr = Transcript()
+        oc = options.to_c()
+        trace = np.ascontiguousarray(trace, dtype=np.uint64)
+        rc = self.lib.zkp_prove_sharded(self.ptr, comm.ptr, air_id, trace.ctypes.data, w, n, pubb, len(pub),
+                                        ctypes.byref(oc), ctypes.byref(out), ctypes.byref(olen), ctypes.byref(tr))
+        self._check(rc, f"zkp_prove_sharded(rank {comm.rank}/{comm.world})")
+        data = ctypes.string_at(out, olen.value)
+        self.lib.zkp_free(out)
+        return data, tr
+
+    def rccl_comm(self, unique_id: bytes, world: int, rank: int) -> "Comm":
+        p = ctypes.c_void_p()
+        self._check(self.lib.zkp_comm_rccl_create(self.ptr, unique_id, world, rank, ctypes.byref(p)),
+                    "zkp_comm_rccl_create")
+        return Comm(p.value)
 
     def prove_device(self, air_id, d_trace, width, n, pub, options):
         shape = np.empty((width, n, 0))

@@ -1,0 +1,144 @@
+// comm.cpp — collective backends of the coset-sharded prover (see comm.hpp).
+#include "comm.hpp"
+
+#include <rccl/rccl.h>
+
+#include <condition_variable>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <vector>
+
+namespace {
+
+void hip_ok(hipError_t e, const char* what) {
+  if (e != hipSuccess) throw CommError(std::string(what) + ": " + hipGetErrorString(e));
+}
+void nccl_ok(ncclResult_t r, const char* what) {
+  if (r != ncclSuccess) throw CommError(std::string(what) + ": " + ncclGetErrorString(r));
+}
+
+// ------------------------------------------------------------------ world 1
+struct SelfComm : zkp_comm {
+  const char* kind() const override { return "self"; }
+  void copy(hipStream_t st, const void* send, void* recv, size_t bytes) {
+    if (send != recv && bytes) hip_ok(hipMemcpyAsync(recv, send, bytes, hipMemcpyDeviceToDevice, st), "self copy");
+  }
+  void all_to_all(hipStream_t st, const void* send, void* recv, size_t b) override { copy(st, send, recv, b); }
+  void all_gather(hipStream_t st, const void* send, void* recv, size_t b) override { copy(st, send, recv, b); }
+};
+
+// ------------------------------------------------------------------ in-process group
+// Ranks are host threads (each with its own zkp_ctx and stream, on one or more
+// devices). A collective publishes the rank's send pointer, meets the others
+// at a barrier, pulls its blocks with device copies, and meets them again so
+// no rank reuses its send buffer while a peer is still reading it.
+struct LocalGroup {
+  int world;
+  std::mutex mu;
+  std::condition_variable cv;
+  int arrived = 0;
+  unsigned long long gen = 0;
+  bool failed = false;
+  std::vector<const void*> ptrs;
+  explicit LocalGroup(int w) : world(w), ptrs(w, nullptr) {}
+  void barrier() {
+    std::unique_lock<std::mutex> lk(mu);
+    if (failed) throw CommError("a peer rank of the local group failed");
+    unsigned long long g = gen;
+    if (++arrived == world) {
+      arrived = 0;
+      gen++;
+      cv.notify_all();
+    } else {
+      cv.wait(lk, [&] { return gen != g || failed; });
+    }
+    if (failed) throw CommError("a peer rank of the local group failed");
+  }
+  void fail() {
+    std::lock_guard<std::mutex> lk(mu);
+    failed = true;
+    cv.notify_all();
+  }
+};
+
+struct LocalComm : zkp_comm {
+  std::shared_ptr<LocalGroup> g;
+  const char* kind() const override { return "local"; }
+  void exchange(hipStream_t st, const void* send, void* recv, size_t bytes, bool a2a) {
+    hip_ok(hipStreamSynchronize(st), "local group: sync before publish");
+    g->ptrs[rank] = send;
+    g->barrier();
+    for (int s = 0; s < world; s++) {
+      const char* src = static_cast<const char*>(g->ptrs[s]) + (a2a ? (size_t)rank * bytes : 0);
+      char* dst = static_cast<char*>(recv) + (size_t)s * bytes;
+      if (src != dst && bytes) hip_ok(hipMemcpyAsync(dst, src, bytes, hipMemcpyDefault, st), "local group copy");
+    }
+    hip_ok(hipStreamSynchronize(st), "local group: sync after copy");
+    g->barrier();
+  }
+  void all_to_all(hipStream_t st, const void* send, void* recv, size_t b) override { exchange(st, send, recv, b, true); }
+  void all_gather(hipStream_t st, const void* send, void* recv, size_t b) override { exchange(st, send, recv, b, false); }
+  void abort() override { g->fail(); }
+};
+
+// ------------------------------------------------------------------ RCCL
+struct RcclComm : zkp_comm {
+  ncclComm_t c = nullptr;
+  const char* kind() const override { return "rccl"; }
+  void all_to_all(hipStream_t st, const void* send, void* recv, size_t b) override {
+    nccl_ok(ncclGroupStart(), "ncclGroupStart");
+    for (int s = 0; s < world; s++) {
+      nccl_ok(ncclSend(static_cast<const char*>(send) + (size_t)s * b, b, ncclUint8, s, c, st), "ncclSend");
+      nccl_ok(ncclRecv(static_cast<char*>(recv) + (size_t)s * b, b, ncclUint8, s, c, st), "ncclRecv");
+    }
+    nccl_ok(ncclGroupEnd(), "ncclGroupEnd");
+  }
+  void all_gather(hipStream_t st, const void* send, void* recv, size_t b) override {
+    nccl_ok(ncclAllGather(send, recv, b, ncclUint8, c, st), "ncclAllGather");
+  }
+  void abort() override {
+    if (c) (void)ncclCommAbort(c);
+    c = nullptr;
+  }
+  ~RcclComm() override {
+    if (c) (void)ncclCommDestroy(c);
+  }
+};
+
+}  // namespace
+
+zkp_comm* make_self_comm() { return new SelfComm(); }
+
+void make_local_group(int world, zkp_comm** out) {
+  auto g = std::make_shared<LocalGroup>(world);
+  for (int r = 0; r < world; r++) {
+    auto* c = new LocalComm();
+    c->rank = r;
+    c->world = world;
+    c->g = g;
+    out[r] = c;
+  }
+}
+
+void rccl_unique_id(unsigned char id[128]) {
+  static_assert(sizeof(ncclUniqueId) == 128, "NCCL_UNIQUE_ID_BYTES");
+  ncclUniqueId u;
+  nccl_ok(ncclGetUniqueId(&u), "ncclGetUniqueId");
+  memcpy(id, &u, sizeof u);
+}
+
+zkp_comm* make_rccl_comm(int device, const unsigned char id[128], int world, int rank) {
+  hip_ok(hipSetDevice(device), "hipSetDevice");
+  ncclUniqueId u;
+  memcpy(&u, id, sizeof u);
+  auto* c = new RcclComm();
+  c->rank = rank;
+  c->world = world;
+  ncclResult_t r = ncclCommInitRank(&c->c, world, u, rank);
+  if (r != ncclSuccess) {
+    delete c;
+    throw CommError(std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
+  }
+  return c;
+}

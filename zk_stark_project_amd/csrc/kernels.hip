@@ -6,7 +6,9 @@
 //  * coefficient arrays: bit-reversed order, scaled by n (output of the
 //    Gentleman-Sande inverse NTT, never permuted);
 //  * LDE matrices: coset-major, column c, coset j, row t at (c*B + j)*n + t,
-//    holding P_c(g * w_N^j * w_n^t) = LDE index i = j + B*t;
+//    holding P_c(g * w_N^j * w_n^t) = LDE index i = j + B*t. A shard owns the
+//    cosets [j0, j0 + Bl) and stores them the same way with B -> Bl, j -> j - j0;
+//  * DEEP / FRI layer evaluations: coset-major too (coset j, position t);
 //  * Merkle trees: nodes[1..2L) of 8-word digests, leaves at nodes[L..2L).
 #include "zkp_internal.hpp"
 #include "blake3.hpp"
@@ -37,6 +39,15 @@ __device__ __forceinline__ felt tw_full(const felt* tw, uint64_t e, uint32_t log
   uint64_t half = 1ull << (logN - 1);
   return e < half ? tw[e] : neg(tw[e - half]);
 }
+
+// domain point of local index q of a coset-major shard: cx[q / n] * w_n^(q % n)
+__device__ __forceinline__ felt point_x(const PointMap& m, uint64_t q) {
+  return mul(m.cx[q >> m.logn], tw_full(m.twn, q & ((1ull << m.logn) - 1), m.logn));
+}
+
+// point handled by (thread, slot k) of a block of EVAL_CH*TPB points: slots
+// are TPB apart so that every load/store of a wave is contiguous
+#define EVAL_POINT(k) ((uint64_t)blockIdx.x * (TPB * EVAL_CH) + (uint64_t)(k) * TPB + threadIdx.x)
 
 __device__ __forceinline__ void store_digest(uint32_t* dst, const uint32_t d[8]) {
   uint4* p = reinterpret_cast<uint4*>(dst);
@@ -316,13 +327,6 @@ __global__ void k_build_coset_scale(felt* S, uint32_t logn, uint32_t B, const fe
   }
 }
 
-__global__ void k_build_ginv(felt* Gi, uint32_t logn, const felt* gilo, const felt* gihi) {
-  uint64_t n = 1ull << logn;
-  for (uint64_t p = blockIdx.x * (uint64_t)TPB + threadIdx.x; p < n; p += (uint64_t)gridDim.x * TPB) {
-    uint32_t k = rev_bits((uint32_t)p, logn);
-    Gi[p] = mul(gilo[k & 2047], gihi[k >> 11]);
-  }
-}
 
 // ------------------------------------------------------------------ hashing
 __global__ __launch_bounds__(TPB) void k_leaf_hash_lde(const felt* __restrict__ lde, uint32_t cols, uint32_t logB,
@@ -388,8 +392,8 @@ struct MerkleArgs {
   const felt* src;
   uint64_t n;       // MODE 0: rows per coset
   uint32_t cols;    // MODE 0: columns; MODE 1: F
-  uint32_t logB;    // MODE 0
-  uint64_t R;       // MODE 1: rows (= leaves)
+  uint32_t logB;    // MODE 0/1: cosets of the (coset-major) source
+  uint64_t R;       // MODE 1: rows per coset (m/16)
   uint32_t* nodes;
   uint64_t L;       // leaves of this (sub)tree level
 };
@@ -402,7 +406,9 @@ __device__ __forceinline__ void merkle_leaf(const MerkleArgs& a, uint64_t i, uin
     const uint64_t cstride = a.n << a.logB;
     b3::hash_felts([&](uint32_t c) { return base[c * cstride]; }, a.cols, d);
   } else if (MODE == 1) {
-    b3::hash_felts([&](uint32_t k) { return a.src[i + k * a.R]; }, a.cols, d);
+    // natural row i = j + B*t' -> coset j, positions t' + k*R
+    const felt* base = a.src + ((i & ((1ull << a.logB) - 1)) * 16) * a.R + (i >> a.logB);
+    b3::hash_felts([&](uint32_t k) { return base[k * a.R]; }, a.cols, d);
   } else {
     load_digest(a.nodes + (a.L + i) * 8, d);
   }
@@ -484,6 +490,65 @@ __global__ __launch_bounds__(256) void k_merkle_lane(MerkleArgs a) {
   lane_subtree<MODE, H>(a, lane << H, root);
 }
 
+// ---- sharded commitments: the rank hashes the rows it owns (cosets
+// [j0, j0+Bl), rows t < rows) and scatters the digests by destination rank
+// (contiguous natural leaf ranges) for the all-to-all:
+// send[((s*Bl + jl)*rr + tl)], s = t / rr, tl = t % rr, rr = rows / R.
+template <int MODE>
+__global__ __launch_bounds__(TPB) void k_leaf_hash_shard(const felt* __restrict__ src, uint64_t n, uint32_t cols,
+                                                         uint32_t logBl, uint32_t logrows, uint32_t logrr,
+                                                         uint32_t* __restrict__ send) {
+  const uint64_t q = blockIdx.x * (uint64_t)TPB + threadIdx.x;
+  const uint64_t rows = 1ull << logrows;
+  if (q >= (rows << logBl)) return;
+  const uint64_t jl = q >> logrows, t = q & (rows - 1);
+  uint32_t d[8];
+  if (MODE == 0) {  // LDE row t of coset jl: (c*Bl + jl)*n + t
+    const felt* base = src + jl * n + t;
+    const uint64_t cstride = n << logBl;
+    b3::hash_felts([&](uint32_t c) { return base[c * cstride]; }, cols, d);
+  } else {  // FRI row: positions t + k*rows of coset jl (16*rows per coset)
+    const felt* base = src + (jl << (logrows + 4)) + t;
+    b3::hash_felts([&](uint32_t k) { return base[k * rows]; }, cols, d);
+  }
+  const uint64_t s = t >> logrr, tl = t & ((1ull << logrr) - 1);
+  store_digest(send + ((((s << logBl) + jl) << logrr) + tl) * 8, d);
+}
+
+// received leaf digests (source-rank-major = global coset j major, B cosets
+// of rr rows) -> natural leaf order of this rank's range: leaf j + B*tl
+__global__ __launch_bounds__(TPB) void k_leaf_unpack(const uint32_t* __restrict__ recv, uint32_t logB, uint32_t logrr,
+                                                     uint32_t* __restrict__ nodes, uint64_t L) {
+  const uint64_t idx = blockIdx.x * (uint64_t)TPB + threadIdx.x;
+  if (idx >= L) return;
+  const uint64_t j = idx >> logrr, tl = idx & ((1ull << logrr) - 1);
+  uint32_t d[8];
+  load_digest(recv + idx * 8, d);
+  store_digest(nodes + (L + j + (tl << logB)) * 8, d);
+}
+
+// ---- composition polynomial from CE-coset evaluations.
+// recv: slices [pl0, pl0 + nR) (bit-reversed positions p) of the CE cosets'
+// Gentleman-Sande inverse NTTs (position p holds n * V_u[rev(p)]); blk[u] =
+// receive block of CE coset u. Si[u*n + p] = (g w_M^u)^-rev(p) turns them into
+// n * U_u[rev(p)], and n * c_m[rev(p)] = sum_u n U_u * coefs[u*C + m] with
+// coefs = w_ce^-um * g^-mn / ce. out[m*nR + pl]: the bit-reversed, n-scaled
+// coefficient layout of the LDE input (directly the columns when nR = n).
+__global__ __launch_bounds__(TPB) void k_comp_dft(const felt* __restrict__ recv, const uint32_t* __restrict__ blk,
+                                                  const felt* __restrict__ Si, const felt* __restrict__ coefs,
+                                                  uint32_t ce, uint32_t C, uint32_t logn, uint64_t p0, uint64_t nR,
+                                                  felt* __restrict__ out) {
+  const uint64_t pl = blockIdx.x * (uint64_t)TPB + threadIdx.x;
+  if (pl >= nR) return;
+  felt U[16];
+  for (uint32_t u = 0; u < ce; u++) U[u] = mul(recv[blk[u] * nR + pl], Si[((uint64_t)u << logn) + p0 + pl]);
+  for (uint32_t m = 0; m < C; m++) {
+    felt acc = zero();
+    for (uint32_t u = 0; u < ce; u++) acc = add(acc, mul(U[u], coefs[u * C + m]));
+    out[m * nR + pl] = acc;
+  }
+}
+
 struct SeedArg {
   uint32_t w[8];
 };
@@ -549,17 +614,17 @@ __device__ __forceinline__ void block_batch_inverse(felt* v, felt* s_pre, felt* 
 }
 
 // Phase 1 of the split batch inversion: product of the denominators
-// (x_s - c0)(x_s - c1) (or (x_s - c0) when !two) of each block's EVAL_CH*TPB
-// points, x_s = g * w_N^(s << xsh). Same point->block mapping as the phase-3 kernels.
-__global__ __launch_bounds__(TPB) void k_den_products(felt g, const felt* __restrict__ tw, uint32_t logN,
-                                                      uint32_t xsh, uint64_t count, felt c0, felt c1, int two,
+// (x_q - c0)(x_q - c1) (or (x_q - c0) when !two) of each block's EVAL_CH*TPB
+// local points q (EVAL_POINT), x_q = point_x(m, q). Same point->block mapping
+// as the phase-3 kernels.
+__global__ __launch_bounds__(TPB) void k_den_products(PointMap m, uint64_t count, felt c0, felt c1, int two,
                                                       felt* __restrict__ prod) {
   __shared__ felt s[TPB];
-  const uint64_t base = (blockIdx.x * (uint64_t)TPB + threadIdx.x) * EVAL_CH;
   felt acc = one();
   static_for<0, EVAL_CH>([&](auto k) {
-    if (base + k < count) {
-      felt x = mul(g, tw_full(tw, (base + k) << xsh, logN));
+    const uint64_t q = EVAL_POINT(k);
+    if (q < count) {
+      felt x = point_x(m, q);
       felt d = sub(x, c0);
       if (two) d = mul(d, sub(x, c1));
       acc = mul(acc, d);
@@ -613,84 +678,84 @@ __global__ __launch_bounds__(1024) void k_invert_products(felt* prod, uint32_t n
   }
 }
 
+// CE point of local index q (CE-coset-major over the shard's CE cosets):
+// CE coset u = u0 + q/n, row t = q % n, CE index s = u + ce*t, LDE coset
+// j = u * B/ce (local jl = j - j0); the frame rows are t and t+1 of that coset.
+struct CePoint {
+  uint64_t s, off, off_next;  // CE index; local LDE offsets of rows t, t+1
+  uint32_t u;
+};
+__device__ __forceinline__ CePoint ce_point(const EvalCommon& c, uint64_t q) {
+  const uint64_t n = 1ull << c.logn;
+  CePoint p;
+  p.u = c.u0 + (uint32_t)(q >> c.logn);
+  const uint64_t t = q & (n - 1);
+  p.s = p.u + (t << c.logce);
+  const uint64_t jl = ((uint64_t)p.u << (c.logB - c.logce)) - c.j0;
+  p.off = jl * n + t;
+  p.off_next = jl * n + ((t + 1) & (n - 1));
+  return p;
+}
+
 __global__ __launch_bounds__(TPB) void k_eval_mimc(EvalCommon c, MimcEvalArgs a, const felt* __restrict__ lde,
                                                    const felt* __restrict__ binv, felt* __restrict__ comp) {
   __shared__ felt s_pre[TPB], s_suf[TPB];
-  const uint64_t M = 1ull << (c.logn + c.logce);
-  const uint64_t base = (blockIdx.x * (uint64_t)TPB + threadIdx.x) * EVAL_CH;
-  const int cnt = base >= M ? 0 : (int)((M - base) < EVAL_CH ? (M - base) : EVAL_CH);
-  const uint64_t n = 1ull << c.logn;
-  const uint32_t sh = c.logB - c.logce;
-  const uint32_t xsh = c.logN - c.logce - c.logn;
+  const uint64_t M = (uint64_t)c.cel << c.logn;
   const uint64_t kmask = (64ull << c.logce) - 1;
   felt tpart[EVAL_CH], bnum[EVAL_CH], den[EVAL_CH];
   static_for<0, EVAL_CH>([&](auto k) {
-    const bool valid = k < cnt;
-    uint64_t s = valid ? base + k : 0;
-    uint64_t idx = s << sh;
-    uint64_t j = idx & ((1ull << c.logB) - 1), t = idx >> c.logB;
-    felt cur = lde[j * n + t];
-    felt nxt = lde[j * n + ((t + 1) & (n - 1))];
-    felt kv = a.kper[s & kmask];
-    felt x = mul(c.g, tw_full(c.tw, s << xsh, c.logN));
+    const uint64_t q0 = EVAL_POINT(k);
+    const bool valid = q0 < M;
+    const uint64_t q = valid ? q0 : 0;
+    const CePoint pt = ce_point(c, q);
+    felt cur = lde[pt.off];
+    felt nxt = lde[pt.off_next];
+    felt kv = a.kper[pt.s & kmask];
+    felt x = point_x(c.pm, q);
     felt u = add(cur, kv);
     felt u2 = sqr(u), u3 = mul(u2, u), u6 = sqr(u3), u7 = mul(u6, u);
     felt tr = mul(a.coef_t, sub(nxt, u7));
     felt e0 = sub(x, one()), e1 = sub(x, c.w_last);
-    tpart[k] = mul(mul(tr, e1), c.zinv[s & ((1ull << c.logce) - 1)]);
+    tpart[k] = mul(mul(tr, e1), c.zinv[pt.u]);
     bnum[k] = add(mul(mul(a.b0, sub(cur, a.v0)), e1), mul(mul(a.b1, sub(cur, a.v1)), e0));
     den[k] = valid ? mul(e0, e1) : one();
   });
   block_batch_inverse(den, s_pre, s_suf, binv[blockIdx.x]);
   static_for<0, EVAL_CH>([&](auto k) {
-    if (k < cnt) comp[base + k] = add(tpart[k], mul(bnum[k], den[k]));
+    const uint64_t q = EVAL_POINT(k);
+    if (q < M) comp[q] = add(tpart[k], mul(bnum[k], den[k]));
   });
 }
 
 __global__ __launch_bounds__(TPB) void k_eval_linear(EvalCommon c, LinearEvalArgs a, const felt* __restrict__ lde,
                                                      const felt* __restrict__ binv, felt* __restrict__ comp) {
   __shared__ felt s_pre[TPB], s_suf[TPB];
-  const uint64_t M = 1ull << (c.logn + c.logce);
-  const uint64_t base = (blockIdx.x * (uint64_t)TPB + threadIdx.x) * EVAL_CH;
-  const int cnt = base >= M ? 0 : (int)((M - base) < EVAL_CH ? (M - base) : EVAL_CH);
-  const uint64_t n = 1ull << c.logn;
-  const uint32_t sh = c.logB - c.logce;
-  const uint32_t xsh = c.logN - c.logce - c.logn;
-  const uint64_t cstride = n << c.logB;
+  const uint64_t M = (uint64_t)c.cel << c.logn;
+  const uint64_t cstride = 1ull << (c.logn + c.logBl);
   felt tpart[EVAL_CH], bnum[EVAL_CH], den[EVAL_CH];
   static_for<0, EVAL_CH>([&](auto k) {
-    const bool valid = k < cnt;
-    uint64_t s = valid ? base + k : 0;
-    uint64_t idx = s << sh;
-    uint64_t j = idx & ((1ull << c.logB) - 1), t = idx >> c.logB;
-    const felt* pc = lde + j * n + t;
-    const felt* pn = lde + j * n + ((t + 1) & (n - 1));
+    const uint64_t q0 = EVAL_POINT(k);
+    const bool valid = q0 < M;
+    const uint64_t q = valid ? q0 : 0;
+    const CePoint pt = ce_point(c, q);
+    const felt* pc = lde + pt.off;
+    const felt* pn = lde + pt.off_next;
     felt tr = zero(), bs = zero();
     for (uint32_t col = 0; col < a.width; col++) {
       felt cur = pc[col * cstride], nxt = pn[col * cstride];
       tr = add(tr, add(mul(a.coefs[col], nxt), mul(a.coefs[a.width + col], cur)));
       bs = add(bs, mul(a.coefs[2 * a.width + col], cur));
     }
-    felt x = mul(c.g, tw_full(c.tw, s << xsh, c.logN));
-    tpart[k] = mul(mul(tr, sub(x, c.w_last)), c.zinv[s & ((1ull << c.logce) - 1)]);
+    felt x = point_x(c.pm, q);
+    tpart[k] = mul(mul(tr, sub(x, c.w_last)), c.zinv[pt.u]);
     bnum[k] = sub(bs, a.bconst);
     den[k] = valid ? sub(x, a.w_bstep) : one();
   });
   block_batch_inverse(den, s_pre, s_suf, binv[blockIdx.x]);
   static_for<0, EVAL_CH>([&](auto k) {
-    if (k < cnt) comp[base + k] = add(tpart[k], mul(bnum[k], den[k]));
+    const uint64_t q = EVAL_POINT(k);
+    if (q < M) comp[q] = add(tpart[k], mul(bnum[k], den[k]));
   });
-}
-
-__global__ void k_segment(const felt* __restrict__ difout, uint32_t logn, uint32_t logce, uint32_t C,
-                          const felt* __restrict__ Gi, const felt* __restrict__ scales, felt* __restrict__ out) {
-  uint64_t n = 1ull << logn, total = (uint64_t)C << logn;
-  for (uint64_t idx = blockIdx.x * (uint64_t)TPB + threadIdx.x; idx < total; idx += (uint64_t)gridDim.x * TPB) {
-    uint32_t h = (uint32_t)(idx >> logn);
-    uint64_t p = idx & (n - 1);
-    felt v = difout[(p << logce) + rev_bits(h, logce)];
-    out[idx] = mul(mul(v, Gi[p]), scales[h]);
-  }
 }
 
 // bit-reversed polynomial evaluation: tree with level multipliers x^(2^l)
@@ -725,43 +790,50 @@ __global__ __launch_bounds__(TPB) void k_eval_bitrev(const felt* __restrict__ ar
   }
 }
 
+// local point q = jl*n + t of the shard's cosets: LDE index i = (j0 + jl) + B*t;
+// the LDE matrices are read at offset q (contiguous), output is coset-major.
 __global__ __launch_bounds__(TPB) void k_deep(DeepArgs a, const felt* __restrict__ binv, felt* __restrict__ out) {
   __shared__ felt s_pre[TPB], s_suf[TPB];
-  const uint64_t N = 1ull << a.logN;
-  const uint64_t base = (blockIdx.x * (uint64_t)TPB + threadIdx.x) * EVAL_CH;
-  const int cnt = base >= N ? 0 : (int)((N - base) < EVAL_CH ? (N - base) : EVAL_CH);
-  const uint64_t n = 1ull << a.logn;
-  const uint64_t cstride = n << a.logB;
+  const uint64_t N = 1ull << (a.logn + a.logBl);
+  const uint64_t cstride = N;
   felt num[EVAL_CH], den[EVAL_CH];
   static_for<0, EVAL_CH>([&](auto k) {
-    const bool valid = k < cnt;
-    uint64_t i = valid ? base + k : 0;
-    uint64_t j = i & ((1ull << a.logB) - 1), t = i >> a.logB;
-    const uint64_t off = j * n + t;
+    const uint64_t q0 = EVAL_POINT(k);
+    const bool valid = q0 < N;
+    const uint64_t off = valid ? q0 : 0;
     felt A = zero(), Bh = zero();
     for (uint32_t c = 0; c < a.w; c++) A = add(A, mul(a.gamma[c], a.tlde[c * cstride + off]));
     for (uint32_t h = 0; h < a.C; h++) Bh = add(Bh, mul(a.gamma[a.w + h], a.clde[h * cstride + off]));
-    felt x = mul(a.g, tw_full(a.tw, i, a.logN));
+    felt x = point_x(a.pm, off);
     felt e1 = sub(x, a.z), e2 = sub(x, a.zg);
     num[k] = add(mul(sub(add(A, Bh), a.kz), e2), mul(sub(A, a.kzg), e1));
     den[k] = valid ? mul(e1, e2) : one();
   });
   block_batch_inverse(den, s_pre, s_suf, binv[blockIdx.x]);
   static_for<0, EVAL_CH>([&](auto k) {
-    if (k < cnt) out[base + k] = mul(num[k], den[k]);
+    const uint64_t q = EVAL_POINT(k);
+    if (q < N) out[q] = mul(num[k], den[k]);
   });
 }
 
 // fold-by-16: u = iDFT16(row) (unscaled), result = (1/16) sum_k u_k beta^k,
-// beta = alpha / x_r; eps_inv[m] = w_16^-m for m < 8, eps_inv[8] = 1/16
-__global__ __launch_bounds__(TPB) void k_fri_fold16(const felt* __restrict__ E, uint64_t R, felt alpha,
-                                                    felt off_inv, const felt* __restrict__ itw_lev,
+// beta = alpha / x_r; eps_inv[m] = w_16^-m for m < 8, eps_inv[8] = 1/16.
+// Layer evaluations are coset-major (coset jl of Bl, m = 16*m16 positions):
+// local row q = jl*m16 + t' is the natural row r = (j0 + jl) + B*t' whose 16
+// values sit at positions t' + k*m16 of the same coset; out is coset-major.
+__global__ __launch_bounds__(TPB) void k_fri_fold16(const felt* __restrict__ E, uint64_t rows, uint32_t logm16,
+                                                    uint32_t j0, uint32_t logB, felt alpha, felt off_inv,
+                                                    const felt* __restrict__ itw_lev,
                                                     const felt* __restrict__ eps_inv, felt* __restrict__ out) {
-  uint64_t r = blockIdx.x * (uint64_t)TPB + threadIdx.x;
-  if (r >= R) return;
+  const uint64_t q = blockIdx.x * (uint64_t)TPB + threadIdx.x;
+  if (q >= rows) return;
+  const uint64_t m16 = 1ull << logm16;
+  const uint64_t jl = q >> logm16, tp = q & (m16 - 1);
+  const uint64_t r = (j0 + jl) + (tp << logB);
+  const felt* src = E + (jl << (logm16 + 4)) + tp;
   felt v[16];
 #pragma unroll
-  for (int k = 0; k < 16; k++) v[k] = E[r + k * R];
+  for (int k = 0; k < 16; k++) v[k] = src[k * m16];
   // Gentleman-Sande, natural in -> bit-reversed out (fully unrolled, constant indices)
 #pragma unroll
   for (int i = 0; i < 8; i++) {
@@ -811,7 +883,7 @@ __global__ __launch_bounds__(TPB) void k_fri_fold16(const felt* __restrict__ E, 
   acc = add(mul(acc, beta), v[4]);
   acc = add(mul(acc, beta), v[8]);
   acc = add(mul(acc, beta), v[0]);
-  out[r] = mul(acc, eps_inv[8]);
+  out[q] = mul(acc, eps_inv[8]);
 }
 
 // multi-segment gather: segment s copies seg[s].count items of seg[s].words
@@ -898,9 +970,24 @@ std::vector<NttPass> ntt_plan(uint32_t logn, bool dit) {
   std::vector<NttPass> out;
   if (logn == 0) return out;
   uint32_t npass = (logn + KMAX - 1) / KMAX;
+  // pass sizes: prefer multiples of 3 (whole radix-8 rounds), largest pass last
+  uint32_t Ks[4] = {0, 0, 0, 0};
+  {
+    uint32_t rem = logn;
+    for (uint32_t p = 0; p < npass; p++) {
+      uint32_t left = npass - p;
+      uint32_t k = (rem + left - 1) / left;
+      if (left > 1) {
+        uint32_t k3 = k / 3 * 3;  // round down to whole radix-8 rounds if the rest still fits
+        if (k3 >= 3 && rem - k3 <= KMAX * (left - 1)) k = k3;
+      }
+      Ks[p] = k;
+      rem -= k;
+    }
+  }
   uint32_t s0 = 0;
   for (uint32_t p = 0; p < npass; p++) {
-    uint32_t K = logn / npass + (p < logn % npass ? 1 : 0);
+    uint32_t K = Ks[p];
     NttPass ps;
     ps.logn = logn;
     ps.s0 = s0;
@@ -968,9 +1055,24 @@ void launch_ntt(Prof& prof, hipStream_t s, const NttBatch& b, uint32_t logn, boo
     (void)hipFuncSetAttribute((const void*)k_ntt8<false, 256>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)maxb);
     attr_set = true;
   }
+  // pass sizes: prefer multiples of 3 (whole radix-8 rounds), largest pass last
+  uint32_t Ks[4] = {0, 0, 0, 0};
+  {
+    uint32_t rem = logn;
+    for (uint32_t p = 0; p < npass; p++) {
+      uint32_t left = npass - p;
+      uint32_t k = (rem + left - 1) / left;
+      if (left > 1) {
+        uint32_t k3 = k / 3 * 3;  // round down to whole radix-8 rounds if the rest still fits
+        if (k3 >= 3 && rem - k3 <= KMAX * (left - 1)) k = k3;
+      }
+      Ks[p] = k;
+      rem -= k;
+    }
+  }
   uint32_t s0 = 0;
   for (uint32_t p = 0; p < npass; p++) {
-    uint32_t K = logn / npass + (p < logn % npass ? 1 : 0);
+    uint32_t K = Ks[p];
     Ntt8Args a;
     bool first = p == 0;
     a.src = first ? b.src : b.dst;
@@ -1030,11 +1132,6 @@ void launch_build_coset_scale(Prof& prof, hipStream_t s, felt* S, uint32_t logn,
                             logn, B, tw, logN, glo, ghi, ninv));
 }
 
-void launch_build_ginv(Prof& prof, hipStream_t s, felt* Gi, uint32_t logn, const felt* gilo, const felt* gihi) {
-  LAUNCH(prof, "build_ginv", s, (double)(1ull << logn) * 16.0,
-         hipLaunchKernelGGL(k_build_ginv, dim3(grid_stride_blocks(1ull << logn)), dim3(TPB), 0, s, Gi, logn, gilo,
-                            gihi));
-}
 
 // tree build by lane-subtree passes: pass 1 hashes leaves and builds H0 levels,
 // later passes build up to 4 levels each from the stored subtree roots.
@@ -1052,7 +1149,7 @@ static void merkle_pass(Prof& prof, hipStream_t s, const MerkleArgs& a, uint32_t
 
 // upper levels: wide levels by lane passes (4 levels each), the narrow top by
 // the LDS-fused kernel (9 levels per launch, parallel tail)
-static void merkle_upper(Prof& prof, hipStream_t s, uint32_t* nodes, uint64_t L) {
+void merkle_upper(Prof& prof, hipStream_t s, uint32_t* nodes, uint64_t L) {
   while (L > 1) {
     MerkleArgs a{};
     a.nodes = nodes;
@@ -1084,10 +1181,13 @@ void launch_merkle_lde(Prof& prof, hipStream_t s, const felt* lde, uint32_t cols
   merkle_upper(prof, s, nodes, L >> H);
 }
 
-void launch_merkle_fri(Prof& prof, hipStream_t s, const felt* E, uint64_t R, uint32_t F, uint32_t* nodes) {
+void launch_merkle_fri(Prof& prof, hipStream_t s, const felt* E, uint64_t m16, uint32_t logB, uint32_t F,
+                       uint32_t* nodes) {
+  const uint64_t R = m16 << logB;
   MerkleArgs a{};
   a.src = E;
-  a.R = R;
+  a.R = m16;
+  a.logB = logB;
   a.cols = F;
   a.nodes = nodes;
   a.L = R;
@@ -1125,20 +1225,19 @@ void launch_grind(Prof& prof, hipStream_t s, const uint32_t* seed_words, uint64_
          hipLaunchKernelGGL(k_grind, dim3(blocks_for(count)), dim3(TPB), 0, s, sa, base, count, bits, result));
 }
 
-static void launch_den_inverse(Prof& prof, hipStream_t s, felt g, const felt* tw, uint32_t logN, uint32_t xsh,
-                               uint64_t count, felt c0, felt c1, int two, felt* prod) {
+static void launch_den_inverse(Prof& prof, hipStream_t s, const PointMap& m, uint64_t count, felt c0, felt c1,
+                               int two, felt* prod) {
   uint32_t nb = blocks_for((count + EVAL_CH - 1) / EVAL_CH);
   LAUNCH(prof, "den_products", s, (double)count * 16.0,
-         hipLaunchKernelGGL(k_den_products, dim3(nb), dim3(TPB), 0, s, g, tw, logN, xsh, count, c0, c1, two, prod));
+         hipLaunchKernelGGL(k_den_products, dim3(nb), dim3(TPB), 0, s, m, count, c0, c1, two, prod));
   LAUNCH(prof, "invert_products", s, (double)nb * 32.0,
          hipLaunchKernelGGL(k_invert_products, dim3(1), dim3(1024), 0, s, prod, nb));
 }
 
 void launch_eval_mimc(Prof& prof, hipStream_t s, const EvalCommon& c, const MimcEvalArgs& a, const felt* lde,
                       felt* comp) {
-  uint64_t M = 1ull << (c.logn + c.logce);
-  if (!a.binv_ready)
-    launch_den_inverse(prof, s, c.g, c.tw, c.logN, c.logN - c.logce - c.logn, M, one(), c.w_last, 1, a.binv);
+  uint64_t M = (uint64_t)c.cel << c.logn;
+  if (!a.binv_ready) launch_den_inverse(prof, s, c.pm, M, one(), c.w_last, 1, a.binv);
   LAUNCH(prof, "eval_mimc", s, (double)M * 32.0,
          hipLaunchKernelGGL(k_eval_mimc, dim3(blocks_for((M + EVAL_CH - 1) / EVAL_CH)), dim3(TPB), 0, s, c, a, lde,
                             a.binv, comp));
@@ -1146,19 +1245,11 @@ void launch_eval_mimc(Prof& prof, hipStream_t s, const EvalCommon& c, const Mimc
 
 void launch_eval_linear(Prof& prof, hipStream_t s, const EvalCommon& c, const LinearEvalArgs& a, const felt* lde,
                         felt* comp) {
-  uint64_t M = 1ull << (c.logn + c.logce);
-  if (!a.binv_ready)
-    launch_den_inverse(prof, s, c.g, c.tw, c.logN, c.logN - c.logce - c.logn, M, a.w_bstep, zero(), 0, a.binv);
+  uint64_t M = (uint64_t)c.cel << c.logn;
+  if (!a.binv_ready) launch_den_inverse(prof, s, c.pm, M, a.w_bstep, zero(), 0, a.binv);
   LAUNCH(prof, "eval_linear", s, (double)M * (a.width * 16.0 + 16.0),
          hipLaunchKernelGGL(k_eval_linear, dim3(blocks_for((M + EVAL_CH - 1) / EVAL_CH)), dim3(TPB), 0, s, c, a, lde,
                             a.binv, comp));
-}
-
-void launch_segment(Prof& prof, hipStream_t s, const felt* difout, uint32_t logn, uint32_t logce, uint32_t C,
-                    const felt* Gi, const felt* scales, felt* out) {
-  LAUNCH(prof, "segment", s, (double)((uint64_t)C << logn) * 48.0,
-         hipLaunchKernelGGL(k_segment, dim3(grid_stride_blocks((uint64_t)C << logn)), dim3(TPB), 0, s, difout, logn,
-                            logce, C, Gi, scales, out));
 }
 
 void launch_eval_bitrev(Prof& prof, hipStream_t s, const felt* arrays, uint32_t narrays, uint32_t logn,
@@ -1172,21 +1263,53 @@ void launch_eval_bitrev(Prof& prof, hipStream_t s, const felt* arrays, uint32_t 
 }
 
 void launch_deep(Prof& prof, hipStream_t s, const DeepArgs& a, felt* out) {
-  uint64_t N = 1ull << a.logN;
-  launch_den_inverse(prof, s, a.g, a.tw, a.logN, 0, N, a.z, a.zg, 1, a.binv);
+  uint64_t N = 1ull << (a.logn + a.logBl);
+  launch_den_inverse(prof, s, a.pm, N, a.z, a.zg, 1, a.binv);
   LAUNCH(prof, "deep", s, (double)N * ((a.w + a.C) * 16.0 + 16.0),
          hipLaunchKernelGGL(k_deep, dim3(blocks_for((N + EVAL_CH - 1) / EVAL_CH)), dim3(TPB), 0, s, a, a.binv, out));
 }
 
-void launch_fri_fold(Prof& prof, hipStream_t s, const felt* E, uint64_t R, uint32_t F, felt alpha, felt off_inv,
-                     const felt* itw, uint32_t logN, uint32_t logD, const felt* eps_inv, felt* out) {
+void launch_fri_fold(Prof& prof, hipStream_t s, const felt* E, uint64_t m16, uint32_t Bl, uint32_t j0,
+                     uint32_t logB, uint32_t F, felt alpha, felt off_inv, const felt* itw, uint32_t logD,
+                     const felt* eps_inv, felt* out) {
   (void)F;  // only 16 is compiled (the reference's fri_folding_factor)
-  (void)logN;
   const felt* lev = itw + ((1ull << (logD - 1)) - 1);  // w_D^-r, r < D/2
-  LAUNCH(prof, "fri_fold16", s, (double)R * (16 * 16.0 + 16.0),
-         hipLaunchKernelGGL(k_fri_fold16, dim3(blocks_for(R)), dim3(TPB), 0, s, E, R, alpha, off_inv, lev,
-                            eps_inv, out));
+  uint32_t logm16 = 0;
+  while ((1ull << logm16) < m16) logm16++;
+  const uint64_t rows = m16 * Bl;
+  LAUNCH(prof, "fri_fold16", s, (double)rows * (16 * 16.0 + 16.0),
+         hipLaunchKernelGGL(k_fri_fold16, dim3(blocks_for(rows)), dim3(TPB), 0, s, E, rows, logm16, j0, logB, alpha,
+                            off_inv, lev, eps_inv, out));
 }
+
+void launch_leaf_hash_shard(Prof& prof, hipStream_t s, int mode, const felt* src, uint64_t n, uint32_t cols,
+                            uint32_t logBl, uint32_t logrows, uint32_t logrr, uint32_t* send) {
+  const uint64_t cnt = 1ull << (logrows + logBl);
+  if (mode == 0)
+    LAUNCH(prof, "leaf_hash_shard", s, (double)cnt * (cols * 16.0 + 32.0),
+           hipLaunchKernelGGL(k_leaf_hash_shard<0>, dim3(blocks_for(cnt)), dim3(TPB), 0, s, src, n, cols, logBl,
+                              logrows, logrr, send));
+  else
+    LAUNCH(prof, "leaf_hash_shard", s, (double)cnt * (cols * 16.0 + 32.0),
+           hipLaunchKernelGGL(k_leaf_hash_shard<1>, dim3(blocks_for(cnt)), dim3(TPB), 0, s, src, n, cols, logBl,
+                              logrows, logrr, send));
+}
+
+void launch_merkle_from_shards(Prof& prof, hipStream_t s, const uint32_t* recv, uint32_t logB, uint32_t logrr,
+                               uint32_t* nodes) {
+  const uint64_t L = 1ull << (logB + logrr);
+  LAUNCH(prof, "leaf_unpack", s, (double)L * 64.0,
+         hipLaunchKernelGGL(k_leaf_unpack, dim3(blocks_for(L)), dim3(TPB), 0, s, recv, logB, logrr, nodes, L));
+  merkle_upper(prof, s, nodes, L);
+}
+
+void launch_comp_dft(Prof& prof, hipStream_t s, const felt* recv, const uint32_t* blk, const felt* Si,
+                     const felt* coefs, uint32_t ce, uint32_t C, uint32_t logn, uint64_t p0, uint64_t nR, felt* out) {
+  LAUNCH(prof, "comp_dft", s, (double)nR * (2 * ce + C) * 16.0,
+         hipLaunchKernelGGL(k_comp_dft, dim3(blocks_for(nR)), dim3(TPB), 0, s, recv, blk, Si, coefs, ce, C, logn, p0,
+                            nR, out));
+}
+
 
 void launch_gather_multi(Prof& prof, hipStream_t s, const GatherSeg* segs, uint32_t nseg, uint64_t max_count,
                          const uint64_t* idx, uint32_t* out, double bytes) {

@@ -8,6 +8,7 @@
 // GPU (kernels.hip); the host only drives the Fiat-Shamir transcript and
 // assembles the proof bytes from the few values the verifier needs.
 #include <algorithm>
+#include <array>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -20,6 +21,7 @@
 
 #include "../../include/zkp.h"
 #include "blake3.hpp"
+#include "comm.hpp"
 #include "zkp_internal.hpp"
 
 using namespace fp;
@@ -473,10 +475,11 @@ struct zkp_ctx {
   felt* tw(uint32_t logN) { return tws(logN) + ((1ull << (logN - 1)) - 1); }
   felt* itw(uint32_t logN) { return itws(logN) + ((1ull << (logN - 1)) - 1); }
 
-  // ---- coset tables for (n, B): S[j*n + p] = n^-1 (g w_N^j)^rev(p) ; Gi[p] = g^-rev(p)
-  std::map<std::pair<uint32_t, uint32_t>, bool> have_coset;
-  void ensure_coset(uint32_t logn, uint32_t logB) {
-    auto key = std::make_pair(logn, logB);
+  // ---- coset tables for (n, B, ce): S[j*n + p] = n^-1 (g w_N^j)^rev(p) (LDE cosets j < B);
+  // Si[u*n + p] = (g w_M^u)^-rev(p) (CE cosets u < ce, M = n*ce)
+  std::map<std::tuple<uint32_t, uint32_t, uint32_t>, bool> have_coset;
+  void ensure_coset(uint32_t logn, uint32_t logB, uint32_t logce) {
+    auto key = std::make_tuple(logn, logB, logce);
     if (have_coset[key]) return;
     uint32_t logN = logn + logB;
     ensure_twiddles(logN);
@@ -499,8 +502,10 @@ struct zkp_ctx {
         felt* S = buf<felt>("S_" + sfx, n << logB);
         launch_build_coset_scale(prof, stream, S, logn, 1u << logB, tw(logN), logN, dlo, dhi, inv(felt_u64(n)));
       } else {
-        felt* Gi = buf<felt>("Gi_" + sfx, n);
-        launch_build_ginv(prof, stream, Gi, logn, dlo, dhi);
+        const uint32_t logM = logn + logce;
+        felt* Si = buf<felt>("Si_" + sfx + "_" + std::to_string(logce), n << logce);
+        launch_build_coset_scale(prof, stream, Si, logn, 1u << logce, itws(logN) + ((1ull << (logM - 1)) - 1), logM,
+                                 dlo, dhi, one());
       }
       sync();
     }
@@ -509,11 +514,19 @@ struct zkp_ctx {
   felt* S(uint32_t logn, uint32_t logB) {
     return reinterpret_cast<felt*>(bufs["S_" + std::to_string(logn) + "_" + std::to_string(logB)].p);
   }
-  felt* Gi(uint32_t logn, uint32_t logB) {
-    return reinterpret_cast<felt*>(bufs["Gi_" + std::to_string(logn) + "_" + std::to_string(logB)].p);
+  felt* Si(uint32_t logn, uint32_t logB, uint32_t logce) {
+    return reinterpret_cast<felt*>(
+        bufs["Si_" + std::to_string(logn) + "_" + std::to_string(logB) + "_" + std::to_string(logce)].p);
+  }
+
+  zkp_comm* self = nullptr;
+  zkp_comm* self_comm() {
+    if (!self) self = make_self_comm();
+    return self;
   }
 
   ~zkp_ctx() {
+    delete self;
     for (auto& kv : bufs)
       if (kv.second.p) (void)hipFree(kv.second.p);
     for (void* p : user_allocs) (void)hipFree(p);
@@ -526,22 +539,68 @@ struct zkp_ctx {
 
 namespace {
 
-// ------------------------------------------------------------------ stage: LDE + commit
-// d_in (w x n natural) -> tcoef (w x n, bitrev, scaled by n), lde (w x B x n coset-major),
-// tree nodes (2N digests) ; returns root
-void lde_commit(zkp_ctx* ctx, const felt* d_in, uint32_t w, uint32_t logn, uint32_t logB, felt* coef, felt* lde,
-                uint32_t* nodes, bool input_is_coef, uint8_t root[32]) {
-  uint32_t logN = logn + logB;
-  uint64_t n = 1ull << logn, N = 1ull << logN;
-  ctx->ensure_coset(logn, logB);
-  if (!input_is_coef) {
-    NttBatch ib{d_in, coef, nullptr, n, n, 1, 1, w};
-    launch_ntt(ctx->prof, ctx->stream, ib, logn, false, ctx->itws(logN), logN);
+// ------------------------------------------------------------------ sharded commitments
+// A Merkle tree over LDE-domain rows. When the rows are sharded over R ranks,
+// rank s builds the subtree of the leaf range [s*L/R, (s+1)*L/R) in `nodes`
+// and every rank holds the top log2(R) levels on the host (`top`, heap
+// layout with top[1] = root and top[R + s] = subtree root of rank s).
+struct TreeShard {
+  uint32_t* nodes = nullptr;  // device subtree (nodes[1..2Lr)), or the whole tree when logR == 0
+  uint64_t Lr = 0;
+  uint32_t logR = 0;
+  std::vector<std::array<uint8_t, 32>> top;
+  // global node k -> host digest (top levels) or (owner rank, local node index)
+  struct Loc {
+    bool host;
+    uint32_t owner;
+    uint64_t local;
+  };
+  Loc locate(uint64_t k) const {
+    uint32_t d = 63 - __builtin_clzll(k);
+    if (d <= logR && logR > 0) return {true, 0, k};
+    uint32_t below = d - logR;
+    uint64_t s = (k >> below) - (1ull << logR);
+    return {false, (uint32_t)s, (1ull << below) + (k & ((1ull << below) - 1))};
   }
-  NttBatch lb{coef, lde, ctx->S(logn, logB), n, n, 1u << logB, 1u << logB, w << logB};
-  launch_ntt(ctx->prof, ctx->stream, lb, logn, true, ctx->tws(logN), logN);
-  launch_merkle_lde(ctx->prof, ctx->stream, lde, w, logB, n, nodes, N);
-  ctx->download(root, nodes + 8, 32);
+};
+
+// commit the rows of a coset-major source held by this rank (cosets [j0, j0+Bl)):
+// mode 0 = LDE rows (cols columns, n rows per coset), mode 1 = FRI rows (16
+// values, 2^logrows rows per coset). Unsharded sources hold all B cosets.
+void commit_rows(zkp_ctx* ctx, zkp_comm* cm, int mode, const felt* src, uint64_t n, uint32_t cols, uint32_t logB,
+                 uint32_t logrows, bool sharded, const std::string& name, TreeShard& tr, uint8_t root[32]) {
+  Prof& pf = ctx->prof;
+  hipStream_t st = ctx->stream;
+  const uint64_t L = 1ull << (logB + logrows);
+  if (!sharded) {
+    tr.logR = 0;
+    tr.Lr = L;
+    tr.nodes = ctx->buf<uint32_t>(name, (size_t)16 * L);
+    if (mode == 0) launch_merkle_lde(pf, st, src, cols, logB, n, tr.nodes, L);
+    else launch_merkle_fri(pf, st, src, 1ull << logrows, logB, 16, tr.nodes);
+    ctx->download(root, tr.nodes + 8, 32);
+    tr.top.assign(2, {});
+    memcpy(tr.top[1].data(), root, 32);
+    return;
+  }
+  const uint32_t R = cm->world, logR = ilog2(R), logBl = logB - logR;
+  const uint32_t logrr = logrows - logR;
+  tr.logR = logR;
+  tr.Lr = 1ull << (logB + logrr);
+  uint32_t* send = ctx->buf<uint32_t>("shard_send", (size_t)8 << (logBl + logrows));
+  uint32_t* recv = ctx->buf<uint32_t>("shard_recv", (size_t)8 << (logBl + logrows));
+  launch_leaf_hash_shard(pf, st, mode, src, n, cols, logBl, logrows, logrr, send);
+  cm->all_to_all(st, send, recv, (size_t)32 << (logBl + logrr));
+  tr.nodes = ctx->buf<uint32_t>(name, (size_t)16 * tr.Lr);
+  launch_merkle_from_shards(pf, st, recv, logB, logrr, tr.nodes);
+  uint32_t* roots = ctx->buf<uint32_t>("shard_roots", (size_t)8 * R);
+  cm->all_gather(st, tr.nodes + 8, roots, 32);
+  std::vector<uint8_t> hr((size_t)32 * R);
+  ctx->download(hr.data(), roots, hr.size());
+  tr.top.assign(2 * R, {});
+  for (uint32_t s = 0; s < R; s++) memcpy(tr.top[R + s].data(), hr.data() + 32 * s, 32);
+  for (uint32_t k = R - 1; k >= 1; k--) merge_bytes(tr.top[2 * k].data(), tr.top[2 * k + 1].data(), tr.top[k].data());
+  memcpy(root, tr.top[1].data(), 32);
 }
 
 // evaluate bit-reversed coefficient arrays (scaled by n) at x0, x1 -> values (x n^-1)
@@ -579,9 +638,9 @@ void ood_eval(zkp_ctx* ctx, const felt* arrays, uint32_t narrays, uint32_t logn,
   }
 }
 
-int prove_impl(zkp_ctx* ctx, int air_id, const felt* d_trace, uint32_t w, uint64_t n, const zkp_felt* pub_elems,
-               uint64_t n_pub, const zkp_proof_options* o, uint8_t** proof, uint64_t* proof_len,
-               zkp_transcript* tr_out) {
+int prove_impl(zkp_ctx* ctx, zkp_comm* cm, int air_id, const felt* d_trace, uint32_t w, uint64_t n,
+               const zkp_felt* pub_elems, uint64_t n_pub, const zkp_proof_options* o, uint8_t** proof,
+               uint64_t* proof_len, zkp_transcript* tr_out) {
   int rc = check_options(o);
   if (rc) return rc;
   if (n < 8 || (n & (n - 1)) || w == 0 || w > 255) return ZKP_ERR_TRACE_SHAPE;
@@ -590,6 +649,11 @@ int prove_impl(zkp_ctx* ctx, int air_id, const felt* d_trace, uint32_t w, uint64
   const uint32_t logn = ilog2(n), logB = ilog2(B), logN = logn + logB;
   const uint64_t N = 1ull << logN;
   if (logN > 32) return ZKP_ERR_TRACE_SHAPE;
+  // coset sharding: rank r owns the LDE cosets [j0, j0 + Bl)
+  const uint32_t R = (uint32_t)cm->world, rank = (uint32_t)cm->rank;
+  if (R == 0 || (R & (R - 1)) || R > B || rank >= R) return ZKP_ERR_ARGUMENT;
+  const uint32_t logR = ilog2(R), Bl = B >> logR, logBl = logB - logR, j0 = rank * Bl;
+  if (R > 1 && logn < logR + 8) return ZKP_ERR_TRACE_SHAPE;  // each rank's Merkle range needs >= 256 rows/coset
   std::vector<felt> pub(n_pub);
   for (uint64_t i = 0; i < n_pub; i++) pub[i] = make(pub_elems[i].lo, pub_elems[i].hi);
   AirDesc air;
@@ -598,7 +662,15 @@ int prove_impl(zkp_ctx* ctx, int air_id, const felt* d_trace, uint32_t w, uint64
   const uint32_t ce = air.ce_blowup(), C = air.comp_cols();
   if (B < ce) return ZKP_ERR_INVALID_OPTIONS;
   const uint32_t logce = ilog2(ce);
-  const uint64_t M = n * ce;
+  if (ce > 16 || C > ce) return ZKP_ERR_UNSUPPORTED_AIR;
+  // CE coset u lives in LDE coset u << (logB - logce); this rank evaluates the CE cosets it holds
+  const uint32_t cstep = logB - logce;
+  auto ce_owner = [&](uint32_t u) { return (u << cstep) / Bl; };
+  auto ce_first = [&](uint32_t s) { uint32_t u = 0; while (u < ce && ce_owner(u) < s) u++; return u; };
+  const uint32_t u0 = ce_first(rank);
+  uint32_t cel = 0;
+  while (u0 + cel < ce && ce_owner(u0 + cel) == rank) cel++;
+  const uint32_t celmax = ce >= R ? ce / R : 1;
   const felt g = felt_u64(3);
   zkp_transcript T;
   memset(&T, 0, sizeof T);
@@ -615,27 +687,46 @@ int prove_impl(zkp_ctx* ctx, int air_id, const felt* d_trace, uint32_t w, uint64
     se.insert(se.end(), pub.begin(), pub.end());
     coin.init(se);
   }
-  ctx->ensure_coset(logn, logB);
+  ctx->ensure_coset(logn, logB, logce);
+  const felt* Sj0 = ctx->S(logn, logB) + (uint64_t)j0 * n;
+  // domain points: coset offsets g*w_N^j (LDE cosets) and g*w_M^u (CE cosets), w_n^t table
+  felt* cx = ctx->buf<felt>("coset_x", B + ce);
+  {
+    std::vector<felt> h(B + ce);
+    felt wN = root_of_unity(logN), wM = root_of_unity(logn + logce);
+    for (uint32_t j = 0; j < B; j++) h[j] = mul(g, pow_u64(wN, j));
+    for (uint32_t u = 0; u < ce; u++) h[B + u] = mul(g, pow_u64(wM, u));
+    ctx->upload(cx, h.data(), h.size() * 16);
+  }
+  const felt* twn = ctx->tws(logN) + ((1ull << (logn - 1)) - 1);
 
-  // 2. trace LDE + commitment (DefaultTraceLde::new)
+  // 2. trace LDE + commitment (DefaultTraceLde::new): interpolation on every
+  // rank, coset LDE of this rank's cosets, sharded row commitment
   felt* coef = ctx->buf<felt>("coef", (size_t)(w + C) * n);
-  felt* tlde = ctx->buf<felt>("tlde", (size_t)w * N);
-  uint32_t* ttree = ctx->buf<uint32_t>("ttree", (size_t)16 * N);
-  lde_commit(ctx, d_trace, w, logn, logB, coef, tlde, ttree, false, T.trace_root);
+  felt* tlde = ctx->buf<felt>("tlde", (size_t)w * Bl * n);
+  TreeShard ttree;
+  {
+    NttBatch ib{d_trace, coef, nullptr, n, n, 1, 1, w};
+    launch_ntt(pf, st, ib, logn, false, ctx->itws(logN), logN);
+    NttBatch lb{coef, tlde, Sj0, n, n, Bl, Bl, w * Bl};
+    launch_ntt(pf, st, lb, logn, true, ctx->tws(logN), logN);
+    commit_rows(ctx, cm, 0, tlde, n, w, logB, logn, R > 1, "ttree", ttree, T.trace_root);
+  }
   coin.reseed(T.trace_root);
   ctx->stage_end("1_trace_commit");
 
   // 3. constraint composition coefficients + evaluation (DefaultConstraintEvaluator)
   const uint32_t ncoef = air.num_t + (uint32_t)air.a_col.size();
   std::vector<felt> cc = draw_coeffs(coin, o->batching_constraints, ncoef);
-  felt* comp = ctx->buf<felt>("comp", M);
-  {
+  felt* comp = ctx->buf<felt>("comp", (size_t)(cel ? cel : 1) * n);
+  if (cel) {
     felt wn = root_of_unity(logn);
     EvalCommon ec;
     ec.logn = logn; ec.logB = logB; ec.logce = logce; ec.logN = logN;
+    ec.u0 = u0; ec.cel = cel; ec.j0 = j0; ec.logBl = logBl;
     ec.g = g;
     ec.w_last = pow_u64(wn, n - 1);
-    ec.tw = ctx->tw(logN);
+    ec.pm = PointMap{cx + B + u0, twn, logn};
     // 1/(x^n - 1) on the CE domain: x^n = g^n * w_ce^s
     std::vector<felt> zinv(ce);
     felt gn = pow_u64(g, n), wce = root_of_unity(logce);
@@ -643,6 +734,8 @@ int prove_impl(zkp_ctx* ctx, int air_id, const felt* d_trace, uint32_t w, uint64
     felt* dz = ctx->buf<felt>("zinv", ce);
     ctx->upload(dz, zinv.data(), ce * 16);
     ec.zinv = dz;
+    const std::string dom = std::to_string(logn) + "_" + std::to_string(logB) + "_" + std::to_string(u0) + "_" +
+                            std::to_string(cel);
     if (air.id == ZKP_AIR_MIMC) {
       // periodic column K over the CE domain: interpolate over <w_64>, evaluate at g^(n/64) * <w_{64 ce}>
       std::vector<felt> kc(64);
@@ -657,9 +750,9 @@ int prove_impl(zkp_ctx* ctx, int air_id, const felt* d_trace, uint32_t w, uint64
       ma.b1 = cc[2]; ma.v1 = air.a_val[1];
       ma.kper = dk;
       // divisor inverses depend only on the domain and the assertion steps: cache per config
-      std::string key = "binv_mimc_" + std::to_string(logn) + "_" + std::to_string(logB);
+      std::string key = "binv_mimc_" + dom;
       ma.binv_ready = ctx->have_cached(key);
-      ma.binv = ctx->buf<felt>(key, M / 2048 + 1);
+      ma.binv = ctx->buf<felt>(key, ((uint64_t)cel * n) / 2048 + 1);
       launch_eval_mimc(pf, st, ec, ma, tlde, comp);
     } else {
       // GlobalUpdate: T = sum_i a^i (k*next_i - k*cur_i - next_{i+60}); B = sum_c b_c (cur_c - v_c)
@@ -681,35 +774,68 @@ int prove_impl(zkp_ctx* ctx, int air_id, const felt* d_trace, uint32_t w, uint64
       la.coefs = dco;
       la.bconst = bconst;
       la.w_bstep = pow_u64(wn, air.a_step[0]);
-      std::string key = "binv_lin_" + std::to_string(logn) + "_" + std::to_string(logB) + "_" +
-                        std::to_string(air.a_step[0]);
+      std::string key = "binv_lin_" + dom + "_" + std::to_string(air.a_step[0]);
       la.binv_ready = ctx->have_cached(key);
-      la.binv = ctx->buf<felt>(key, M / 2048 + 1);
+      la.binv = ctx->buf<felt>(key, ((uint64_t)cel * n) / 2048 + 1);
       launch_eval_linear(pf, st, ec, la, tlde, comp);
     }
   }
 
-  // 4. composition polynomial + commitment (DefaultConstraintCommitment)
+  // 4. composition polynomial + commitment (CompositionPoly::new +
+  // DefaultConstraintCommitment): per-CE-coset interpolation, exchange of
+  // coefficient slices, ce-point DFT per coefficient, all-gather, coset LDE
   felt* acoef = coef + (size_t)w * n;
-  felt* clde = ctx->buf<felt>("clde", (size_t)C * N);
-  uint32_t* ctree = ctx->buf<uint32_t>("ctree", (size_t)16 * N);
+  felt* clde = ctx->buf<felt>("clde", (size_t)C * Bl * n);
+  TreeShard ctree;
   {
-    NttBatch ib{comp, comp, nullptr, M, M, 1, 1, 1};
-    launch_ntt(pf, st, ib, logn + logce, false, ctx->itws(logN), logN);
-    std::vector<felt> sc(C);
-    felt nm = mul(felt_u64(n), inv(felt_u64(M)));
-    felt ginv_n = inv(pow_u64(g, n));
-    felt acc = nm;
-    for (uint32_t h = 0; h < C; h++) { sc[h] = acc; acc = mul(acc, ginv_n); }
-    felt* dsc = ctx->buf<felt>("seg_scales", C);
-    ctx->upload(dsc, sc.data(), C * 16);
-    launch_segment(pf, st, comp, logn, logce, C, ctx->Gi(logn, logB), dsc, acoef);
-    lde_commit(ctx, nullptr, C, logn, logB, acoef, clde, ctree, true, T.constraint_root);
+    // this rank's slice of bit-reversed coefficient positions: [p0, p0 + nR)
+    const uint64_t nR = n >> logR, p0 = (uint64_t)rank * nR;
+    if (cel) {
+      NttBatch ib{comp, comp, nullptr, n, n, 1, 1, cel};
+      launch_ntt(pf, st, ib, logn, false, ctx->itws(logN), logN);
+    }
+    felt* recv = comp;  // world 1: the rank holds every CE coset in full
+    if (R > 1) {
+      // send block s = positions [s*nR, (s+1)*nR) of every owned CE coset
+      felt* send = ctx->buf<felt>("comp_send", (size_t)celmax * n);
+      recv = ctx->buf<felt>("comp_recv", (size_t)celmax * n);
+      for (uint32_t ul = 0; ul < cel; ul++)
+        HIP_CHECK(hipMemcpy2DAsync(send + (size_t)ul * nR, (size_t)celmax * nR * 16, comp + (size_t)ul * n, nR * 16,
+                                   nR * 16, R, hipMemcpyDeviceToDevice, st));
+      cm->all_to_all(st, send, recv, (size_t)celmax * nR * 16);
+    }
+    // coefs[u*C + m] = w_ce^-um * g^-mn / ce ; blk[u] = receive block holding CE coset u
+    std::vector<felt> dc((size_t)ce * C);
+    felt wce_inv = inv(root_of_unity(logce)), ce_inv = inv(felt_u64(ce)), gn_inv = inv(pow_u64(g, n));
+    for (uint32_t u = 0; u < ce; u++)
+      for (uint32_t m = 0; m < C; m++)
+        dc[(size_t)u * C + m] = mul(mul(pow_u64(wce_inv, (uint64_t)u * m), pow_u64(gn_inv, m)), ce_inv);
+    std::vector<uint32_t> blk(ce);
+    for (uint32_t u = 0; u < ce; u++) {
+      uint32_t s = ce_owner(u);
+      blk[u] = s * celmax + (u - ce_first(s));
+    }
+    felt* dcoefs = ctx->buf<felt>("comp_dft_coefs", dc.size());
+    uint32_t* dblk = ctx->buf<uint32_t>("comp_dft_blk", ce);
+    ctx->upload(dcoefs, dc.data(), dc.size() * 16);
+    ctx->upload(dblk, blk.data(), blk.size() * 4);
+    felt* slice = R > 1 ? ctx->buf<felt>("comp_ag_send", (size_t)C * nR) : acoef;
+    launch_comp_dft(pf, st, recv, dblk, ctx->Si(logn, logB, logce), dcoefs, ce, C, logn, p0, nR, slice);
+    if (R > 1) {
+      felt* ag = ctx->buf<felt>("comp_ag_recv", (size_t)C * n);
+      cm->all_gather(st, slice, ag, (size_t)C * nR * 16);
+      for (uint32_t m = 0; m < C; m++)  // [s][m][pl] -> column m, positions s*nR + pl
+        HIP_CHECK(hipMemcpy2DAsync(acoef + (size_t)m * n, nR * 16, ag + (size_t)m * nR, (size_t)C * nR * 16, nR * 16,
+                                   R, hipMemcpyDeviceToDevice, st));
+    }
+    NttBatch lb{acoef, clde, Sj0, n, n, Bl, Bl, C * Bl};
+    launch_ntt(pf, st, lb, logn, true, ctx->tws(logN), logN);
+    commit_rows(ctx, cm, 0, clde, n, C, logB, logn, R > 1, "ctree", ctree, T.constraint_root);
   }
   coin.reseed(T.constraint_root);
   ctx->stage_end("2_constraints_commit");
 
-  // 5. OOD frame
+  // 5. OOD frame (every rank holds all trace and composition coefficients)
   felt z = coin.draw();
   T.z.lo = z.lo; T.z.hi = z.hi;
   felt zg = mul(z, root_of_unity(logn));
@@ -725,9 +851,9 @@ int prove_impl(zkp_ctx* ctx, int air_id, const felt* d_trace, uint32_t w, uint64
   coin.reseed(dg);
   ctx->stage_end("3_ood");
 
-  // 6. DEEP composition evaluations over the LDE domain
+  // 6. DEEP composition evaluations over this rank's cosets (coset-major)
   std::vector<felt> gam = draw_coeffs(coin, o->batching_deep, w + C);
-  felt* deep = ctx->buf<felt>("deep", N);
+  felt* deep = ctx->buf<felt>("deep", (size_t)Bl * n);
   {
     felt kz = zero(), kzg = zero();
     for (uint32_t c = 0; c < w; c++) { kz = add(kz, mul(gam[c], oz[c])); kzg = add(kzg, mul(gam[c], ozg[c])); }
@@ -736,30 +862,36 @@ int prove_impl(zkp_ctx* ctx, int air_id, const felt* d_trace, uint32_t w, uint64
     ctx->upload(dg2, gam.data(), gam.size() * 16);
     DeepArgs da;
     da.w = w; da.C = C; da.logB = logB; da.logn = logn; da.logN = logN;
+    da.j0 = j0; da.logBl = logBl;
     da.tlde = tlde; da.clde = clde; da.gamma = dg2;
     da.z = z; da.zg = zg; da.kz = kz; da.kzg = kzg; da.g = g;
-    da.tw = ctx->tw(logN);
-    da.binv = ctx->buf<felt>("binv", N / 2048 + 1);
+    da.pm = PointMap{cx + j0, twn, logn};
+    da.binv = ctx->buf<felt>("binv", ((uint64_t)Bl * n) / 2048 + 1);
     launch_deep(pf, st, da, deep);
   }
   ctx->stage_end("4_deep_launch");
 
-  // 7. FRI layers (FriProver::build_layers), folding factor 16
+  // 7. FRI layers (FriProver::build_layers), folding factor 16. Layers stay
+  // coset-sharded while each rank's Merkle range has >= 16 rows per coset,
+  // then are all-gathered and finished identically on every rank.
   uint32_t L = 0;
   {
     uint64_t D = N, maxrem = (uint64_t)(o->fri_remainder_max_degree + 1) * B;
     while (D > maxrem) { D /= F; L++; }
   }
+  struct Layer {
+    felt* E;
+    uint64_t m;    // positions per coset
+    uint32_t Bc, jc;
+    bool sharded;
+    TreeShard tree;
+  };
+  std::vector<Layer> layers(L + 1);
   std::vector<felt> remainder;
-  std::vector<felt*> layer_evals(L + 1);
-  std::vector<uint32_t*> layer_trees(L);
-  std::vector<uint64_t> layer_size(L + 1);
   {
-    // all later layers in one buffer; trees in one buffer
-    uint64_t tot_e = 0, tot_t = 0, D = N;
-    for (uint32_t l = 0; l < L; l++) { tot_e += D / F; tot_t += 2 * (D / F); D /= F; }
+    uint64_t tot_e = 0, D = N;
+    for (uint32_t l = 0; l < L; l++) { tot_e += D / F; D /= F; }
     felt* fe = ctx->buf<felt>("fri_evals", tot_e + 1);
-    uint32_t* ft = ctx->buf<uint32_t>("fri_trees", 8 * (tot_t + 1));
     std::vector<felt> eps(9);
     felt einv = inv(root_of_unity(4));
     eps[0] = one();
@@ -767,31 +899,45 @@ int prove_impl(zkp_ctx* ctx, int air_id, const felt* d_trace, uint32_t w, uint64
     eps[8] = inv(felt_u64(16));
     felt* deps = ctx->buf<felt>("eps_inv", 9);
     ctx->upload(deps, eps.data(), 9 * 16);
-    layer_evals[0] = deep;
+    felt* E = deep;
+    uint64_t m = n, eo = 0;
+    uint32_t Bc = Bl, jc = j0;
+    bool sh = R > 1;
     D = N;
     felt off = g;
-    uint64_t eo = 0, to = 0;
+    auto replicate = [&](uint32_t l) {  // all-gather the layer: rank blocks = coset blocks in order
+      felt* full = ctx->buf<felt>("fri_full_" + std::to_string(l), (size_t)B * m);
+      cm->all_gather(st, E, full, (size_t)Bl * m * 16);
+      E = full;
+      Bc = B;
+      jc = 0;
+      sh = false;
+    };
     for (uint32_t l = 0; l < L; l++) {
-      uint64_t R = D / F;
-      layer_size[l] = D;
-      uint32_t* nodes = ft + 8 * to;
-      layer_trees[l] = nodes;
-      launch_merkle_fri(pf, st, layer_evals[l], R, F, nodes);
-      ctx->download(T.fri_roots[l], nodes + 8, 32);
+      const uint64_t m16 = m / F;
+      if (sh && (m16 >> logR) < 16) replicate(l);
+      Layer& ly = layers[l];
+      ly.E = E; ly.m = m; ly.Bc = Bc; ly.jc = jc; ly.sharded = sh;
+      commit_rows(ctx, cm, 1, E, 0, F, logB, ilog2(m16), sh, "ftree_" + std::to_string(l), ly.tree,
+                  T.fri_roots[l]);
       coin.reseed(T.fri_roots[l]);
       felt alpha = coin.draw();
       felt* nxt = fe + eo;
-      launch_fri_fold(pf, st, layer_evals[l], R, F, alpha, inv(off), ctx->itws(logN), logN, ilog2(D), deps, nxt);
-      layer_evals[l + 1] = nxt;
-      eo += R;
-      to += 2 * R;
-      D = R;
+      launch_fri_fold(pf, st, E, m16, Bc, jc, logB, F, alpha, inv(off), ctx->itws(logN), ilog2(D), deps, nxt);
+      eo += (uint64_t)Bc * m16;
+      E = nxt;
+      m = m16;
+      D /= F;
       off = pow_u64(off, F);
     }
-    layer_size[L] = D;
+    if (sh) replicate(L);
+    layers[L].E = E; layers[L].m = m; layers[L].Bc = B; layers[L].jc = 0; layers[L].sharded = false;
     // remainder polynomial (FriProver::set_remainder): interpolate the last layer, keep D/B coefficients
+    std::vector<felt> cm_vals((size_t)B * m);
+    ctx->download(cm_vals.data(), E, cm_vals.size() * 16);
     remainder.resize(D);
-    ctx->download(remainder.data(), layer_evals[L], D * 16);
+    for (uint64_t j = 0; j < B; j++)
+      for (uint64_t t = 0; t < m; t++) remainder[j + B * t] = cm_vals[j * m + t];
     host_interpolate(remainder, off);
     remainder.resize(D / B);
     hash_elements(remainder.data(), remainder.size(), T.remainder_commitment);
@@ -800,7 +946,7 @@ int prove_impl(zkp_ctx* ctx, int air_id, const felt* d_trace, uint32_t w, uint64
   }
   ctx->stage_end("5_fri");
 
-  // 8. grinding: minimum nonce >= 1
+  // 8. grinding: minimum nonce >= 1 (every rank finds the same nonce)
   uint64_t nonce = 0;
   if (o->grinding_factor == 0) {
     nonce = 1;
@@ -833,88 +979,135 @@ int prove_impl(zkp_ctx* ctx, int air_id, const felt* d_trace, uint32_t w, uint64
   for (uint64_t i = 0; i < np; i++) T.query_positions[i] = pos[i];
   T.num_composition_columns = C;
 
-  // gather all opened values and Merkle nodes
-  std::vector<uint64_t> fidx_t, fidx_c;
-  for (uint64_t p : pos) {
-    uint64_t j = p & (B - 1), t = p >> logB;
-    for (uint32_t c = 0; c < w; c++) fidx_t.push_back(((uint64_t)c * B + j) * n + t);
-    for (uint32_t h = 0; h < C; h++) fidx_c.push_back(((uint64_t)h * B + j) * n + t);
-  }
-  BatchPlan bt = plan_batch(N, pos), bc = plan_batch(N, pos);
-  std::vector<std::vector<uint64_t>> fpos(L);
-  std::vector<BatchPlan> bf(L);
-  std::vector<std::vector<uint64_t>> fidx(L);
-  {
-    std::vector<uint64_t> cur = pos;
-    for (uint32_t l = 0; l < L; l++) {
-      uint64_t R = layer_size[l] / F;
-      fpos[l] = fold_positions(cur, R);
-      bf[l] = plan_batch(R, fpos[l]);
-      for (uint64_t r : fpos[l])
-        for (uint32_t k = 0; k < F; k++) fidx[l].push_back(r + k * R);
-      cur = fpos[l];
-    }
-  }
-  // one batched gather for every opened value and Merkle path node
+  // Openings: every item is (owner rank, local index) or a host-side top node.
+  // Each rank gathers all items from its own memory (index 0 for items it does
+  // not own), the gathered buffers are all-gathered, and every item is taken
+  // from its owner's copy.
   struct SegPlan {
     const void* src;
     std::vector<uint64_t> idx;
+    std::vector<int32_t> owner;  // -1: host top node (value in host_dig)
+    std::vector<const uint8_t*> host_dig;
     uint32_t words;
   };
-  std::vector<SegPlan> plan;
-  auto path_idx = [](const BatchPlan& bp) {
-    std::vector<uint64_t> idx;
-    for (auto& pth : bp.paths) idx.insert(idx.end(), pth.begin(), pth.end());
-    return idx;
+  auto row_owner = [&](uint64_t j) -> uint32_t { return R > 1 ? (uint32_t)(j / Bl) : 0; };
+  auto lde_values = [&](const felt* src, uint32_t cols) {
+    SegPlan sp{src, {}, {}, {}, 4};
+    for (uint64_t p : pos) {
+      uint64_t j = p & (B - 1), t = p >> logB;
+      uint32_t ow = row_owner(j);
+      for (uint32_t c = 0; c < cols; c++) {
+        sp.idx.push_back(ow == rank ? ((uint64_t)c * Bl + (j - j0)) * n + t : 0);
+        sp.owner.push_back((int32_t)ow);
+        sp.host_dig.push_back(nullptr);
+      }
+    }
+    return sp;
   };
-  plan.push_back({tlde, fidx_t, 4});
-  plan.push_back({ttree, path_idx(bt), 8});
-  plan.push_back({clde, fidx_c, 4});
-  plan.push_back({ctree, path_idx(bc), 8});
-  for (uint32_t l = 0; l < L; l++) {
-    plan.push_back({layer_evals[l], fidx[l], 4});
-    plan.push_back({layer_trees[l], path_idx(bf[l]), 8});
+  auto path_nodes = [&](const TreeShard& tr, const BatchPlan& bp) {
+    SegPlan sp{tr.nodes, {}, {}, {}, 8};
+    for (auto& pth : bp.paths)
+      for (uint64_t k : pth) {
+        TreeShard::Loc lc = tr.locate(k);
+        if (lc.host) {
+          sp.idx.push_back(0);
+          sp.owner.push_back(-1);
+          sp.host_dig.push_back(tr.top[lc.local].data());
+        } else {
+          sp.idx.push_back(lc.owner == (tr.logR ? rank : 0u) ? lc.local : 0);
+          sp.owner.push_back(tr.logR ? (int32_t)lc.owner : (int32_t)rank);
+          sp.host_dig.push_back(nullptr);
+        }
+      }
+    return sp;
+  };
+  BatchPlan bt = plan_batch(N, pos), bc = plan_batch(N, pos);
+  std::vector<std::vector<uint64_t>> fpos(L);
+  std::vector<BatchPlan> bf(L);
+  std::vector<SegPlan> plan;
+  plan.push_back(lde_values(tlde, w));
+  plan.push_back(path_nodes(ttree, bt));
+  plan.push_back(lde_values(clde, C));
+  plan.push_back(path_nodes(ctree, bc));
+  {
+    std::vector<uint64_t> cur = pos;
+    for (uint32_t l = 0; l < L; l++) {
+      const Layer& ly = layers[l];
+      const uint64_t m16 = ly.m / F, Rows = (uint64_t)B * m16;
+      fpos[l] = fold_positions(cur, Rows);
+      bf[l] = plan_batch(Rows, fpos[l]);
+      SegPlan sp{ly.E, {}, {}, {}, 4};
+      for (uint64_t r : fpos[l])
+        for (uint32_t k = 0; k < F; k++) {
+          uint64_t i = r + k * Rows;  // natural index in the layer
+          uint64_t j = i & (B - 1), tt = i >> logB;
+          uint32_t ow = ly.sharded ? (uint32_t)(j / Bl) : rank;
+          sp.idx.push_back(ow == rank ? (j - ly.jc) * ly.m + tt : 0);
+          sp.owner.push_back((int32_t)ow);
+          sp.host_dig.push_back(nullptr);
+        }
+      plan.push_back(sp);
+      plan.push_back(path_nodes(ly.tree, bf[l]));
+      cur = fpos[l];
+    }
   }
   std::vector<GatherSeg> segs;
   std::vector<uint64_t> all_idx;
   uint64_t out_words = 0, max_count = 1;
   for (auto& sp : plan) {
-    GatherSeg g;
-    g.src = sp.src;
-    g.idx_off = all_idx.size();
-    g.count = sp.idx.size();
-    g.out_off = out_words;
-    g.words = sp.words;
-    g.pad = 0;
+    GatherSeg gs;
+    gs.src = sp.src;
+    gs.idx_off = all_idx.size();
+    gs.count = sp.idx.size();
+    gs.out_off = out_words;
+    gs.words = sp.words;
+    gs.pad = 0;
     all_idx.insert(all_idx.end(), sp.idx.begin(), sp.idx.end());
-    out_words += g.count * sp.words;
-    max_count = std::max<uint64_t>(max_count, g.count);
-    segs.push_back(g);
+    out_words += gs.count * sp.words;
+    max_count = std::max<uint64_t>(max_count, gs.count);
+    segs.push_back(gs);
   }
   size_t seg_bytes = segs.size() * sizeof(GatherSeg), idx_bytes = all_idx.size() * 8;
   size_t up_bytes = seg_bytes + idx_bytes, down_bytes = out_words * 4;
-  uint8_t* hp = (uint8_t*)ctx->pinned(std::max(up_bytes, down_bytes) + 64);
+  uint8_t* hp = (uint8_t*)ctx->pinned(std::max(up_bytes, down_bytes * R) + 64);
   memcpy(hp, segs.data(), seg_bytes);
   memcpy(hp + seg_bytes, all_idx.data(), idx_bytes);
   uint8_t* dup = ctx->buf<uint8_t>("gather_in", up_bytes + 16);
   uint32_t* dout = ctx->buf<uint32_t>("gather_out", out_words + 4);
+  uint32_t* dall = R > 1 ? ctx->buf<uint32_t>("gather_all", out_words * R + 4) : dout;
   HIP_CHECK(hipMemcpyAsync(dup, hp, up_bytes, hipMemcpyHostToDevice, st));
   launch_gather_multi(pf, st, (const GatherSeg*)dup, (uint32_t)segs.size(), max_count,
                       (const uint64_t*)(dup + seg_bytes), dout, (double)down_bytes * 2);
-  HIP_CHECK(hipMemcpyAsync(hp, dout, down_bytes, hipMemcpyDeviceToHost, st));
+  if (R > 1) cm->all_gather(st, dout, dall, down_bytes);
+  HIP_CHECK(hipMemcpyAsync(hp, dall, down_bytes * R, hipMemcpyDeviceToHost, st));
   ctx->sync();
   std::vector<uint32_t> gathered(out_words);
-  memcpy(gathered.data(), hp, down_bytes);
+  {
+    const uint32_t* all = reinterpret_cast<const uint32_t*>(hp);
+    for (size_t si = 0; si < plan.size(); si++) {
+      const SegPlan& sp = plan[si];
+      const GatherSeg& gs = segs[si];
+      for (size_t it = 0; it < sp.idx.size(); it++) {
+        uint32_t* dst = gathered.data() + gs.out_off + it * sp.words;
+        if (sp.owner[it] < 0) {
+          memcpy(dst, sp.host_dig[it], 32);
+        } else {
+          uint32_t ow = R > 1 ? (uint32_t)sp.owner[it] : 0;
+          memcpy(dst, all + (size_t)ow * out_words + gs.out_off + it * sp.words, sp.words * 4);
+        }
+      }
+    }
+  }
   size_t seg_cursor = 0;
   auto next_vals = [&]() {
-    const GatherSeg& g = segs[seg_cursor++];
-    std::vector<felt> v(g.count);
-    memcpy(v.data(), gathered.data() + g.out_off, g.count * 16);
+    const GatherSeg& gs = segs[seg_cursor++];
+    std::vector<felt> v(gs.count);
+    memcpy(v.data(), gathered.data() + gs.out_off, gs.count * 16);
     return v;
   };
   auto next_digests = [&]() {
-    const GatherSeg& g = segs[seg_cursor++];
-    return std::vector<uint32_t>(gathered.begin() + g.out_off, gathered.begin() + g.out_off + g.count * 8);
+    const GatherSeg& gs = segs[seg_cursor++];
+    return std::vector<uint32_t>(gathered.begin() + gs.out_off, gathered.begin() + gs.out_off + gs.count * 8);
   };
   auto write_batch = [&](Writer& wr, const BatchPlan& bp, const std::vector<uint32_t>& d) {
     wr.u8((uint8_t)bp.depth);
@@ -991,6 +1184,10 @@ int guarded(zkp_ctx* ctx, F&& f) {
   } catch (const std::bad_alloc&) {
     ctx->err = "host out of memory";
     return ZKP_ERR_OOM;
+  } catch (const CommError& e) {
+    ctx->err = std::string("collective failed: ") + e.what();
+    ctx->prof.pending.clear();
+    return ZKP_ERR_DEVICE;
   } catch (...) {
     ctx->err = "unknown failure";
     return ZKP_ERR_DEVICE;
@@ -1040,7 +1237,8 @@ int zkp_prove_device(zkp_ctx* ctx, zkp_air_id air, const void* d_trace, uint32_t
     ctx->err.clear();
     HIP_CHECK(hipSetDevice(ctx->device));
     if (!d_trace) return (int)ZKP_ERR_ARGUMENT;
-    return prove_impl(ctx, air, (const felt*)d_trace, width, n, pub, n_pub, opts, proof, proof_len, transcript);
+    return prove_impl(ctx, ctx->self_comm(), air, (const felt*)d_trace, width, n, pub, n_pub, opts, proof,
+                      proof_len, transcript);
   });
 }
 
@@ -1054,9 +1252,59 @@ int zkp_prove(zkp_ctx* ctx, zkp_air_id air, const zkp_felt* trace, uint32_t widt
     if (n < 8 || (n & (n - 1)) || width == 0 || width > 255) return (int)ZKP_ERR_TRACE_SHAPE;
     felt* d = ctx->buf<felt>("trace_in", (size_t)width * n);
     ctx->upload(d, trace, (size_t)width * n * 16);
-    return prove_impl(ctx, air, d, width, n, pub, n_pub, opts, proof, proof_len, transcript);
+    return prove_impl(ctx, ctx->self_comm(), air, d, width, n, pub, n_pub, opts, proof, proof_len, transcript);
   });
 }
+
+int zkp_prove_sharded(zkp_ctx* ctx, zkp_comm* comm, zkp_air_id air, const zkp_felt* trace, uint32_t width,
+                      uint64_t n, const zkp_felt* pub, uint64_t n_pub, const zkp_proof_options* opts, uint8_t** proof,
+                      uint64_t* proof_len, zkp_transcript* transcript) {
+  int rc = guarded(ctx, [&] {
+    ctx->err.clear();
+    HIP_CHECK(hipSetDevice(ctx->device));
+    if (!trace || !comm) return (int)ZKP_ERR_ARGUMENT;
+    if (n < 8 || (n & (n - 1)) || width == 0 || width > 255) return (int)ZKP_ERR_TRACE_SHAPE;
+    felt* d = ctx->buf<felt>("trace_in", (size_t)width * n);
+    ctx->upload(d, trace, (size_t)width * n * 16);
+    return prove_impl(ctx, comm, air, d, width, n, pub, n_pub, opts, proof, proof_len, transcript);
+  });
+  // a rank that fails (argument checks included) releases peers blocked in a collective
+  if (rc && comm) comm->abort();
+  return rc;
+}
+
+int zkp_comm_local_group(int world, zkp_comm** comms) {
+  if (!comms || world < 1 || world > 64) return ZKP_ERR_ARGUMENT;
+  try {
+    make_local_group(world, comms);
+  } catch (...) {
+    return ZKP_ERR_OOM;
+  }
+  return ZKP_OK;
+}
+
+int zkp_comm_rccl_unique_id(uint8_t id[128]) {
+  if (!id) return ZKP_ERR_ARGUMENT;
+  try {
+    rccl_unique_id(id);
+  } catch (...) {
+    return ZKP_ERR_DEVICE;
+  }
+  return ZKP_OK;
+}
+
+int zkp_comm_rccl_create(zkp_ctx* ctx, const uint8_t id[128], int world, int rank, zkp_comm** out) {
+  return guarded(ctx, [&] {
+    if (!id || !out || world < 1 || rank < 0 || rank >= world) return (int)ZKP_ERR_ARGUMENT;
+    *out = make_rccl_comm(ctx->device, id, world, rank);
+    return 0;
+  });
+}
+
+void zkp_comm_destroy(zkp_comm* comm) { delete comm; }
+
+int zkp_comm_rank(const zkp_comm* comm) { return comm ? comm->rank : -1; }
+int zkp_comm_world(const zkp_comm* comm) { return comm ? comm->world : -1; }
 
 int zkp_device_alloc(zkp_ctx* ctx, uint64_t bytes, void** d_ptr) {
   return guarded(ctx, [&] {
@@ -1106,8 +1354,14 @@ int zkp_trace_lde_commit(zkp_ctx* ctx, const zkp_felt* trace, uint32_t w, uint64
     ctx->upload(d, trace, (size_t)w * n * 16);
     felt* coef = ctx->buf<felt>("coef", (size_t)w * n);
     felt* lde = ctx->buf<felt>("tlde", (size_t)w * N);
-    uint32_t* tree = ctx->buf<uint32_t>("ttree", (size_t)16 * N);
-    lde_commit(ctx, d, w, logn, logB, coef, lde, tree, false, root);
+    ctx->ensure_coset(logn, logB, 1);
+    const uint32_t logN = logn + logB;
+    NttBatch ib{d, coef, nullptr, n, n, 1, 1, w};
+    launch_ntt(ctx->prof, ctx->stream, ib, logn, false, ctx->itws(logN), logN);
+    NttBatch lb{coef, lde, ctx->S(logn, logB), n, n, blowup, blowup, w * blowup};
+    launch_ntt(ctx->prof, ctx->stream, lb, logn, true, ctx->tws(logN), logN);
+    TreeShard tr;
+    commit_rows(ctx, ctx->self_comm(), 0, lde, n, w, logB, logn, false, "ttree", tr, root);
     if (lde_out) {
       std::vector<felt> h((size_t)w * N);
       ctx->download(h.data(), lde, h.size() * 16);

@@ -53,11 +53,10 @@ void launch_ntt(Prof& prof, hipStream_t s, const NttBatch& b, uint32_t logn, boo
 void launch_build_levels(Prof& prof, hipStream_t s, felt* tab, uint32_t top);
 void launch_expand_powers(Prof& prof, hipStream_t s, felt* out, uint64_t count, const felt* lo_tab,
                           const felt* hi_tab);
-// S[j*n + p] = ninv * (g * w_N^j)^rev(p)   (j < B)
+// S[j*n + p] = ninv * (g * w_N^j)^rev(p)   (j < B; with g^-1 powers and the
+// inverse table of a 2^logN domain this builds the inverse coset tables)
 void launch_build_coset_scale(Prof& prof, hipStream_t s, felt* S, uint32_t logn, uint32_t B,
                               const felt* tw, uint32_t logN, const felt* glo, const felt* ghi, felt ninv);
-// Gi[p] = g^-rev(p)
-void launch_build_ginv(Prof& prof, hipStream_t s, felt* Gi, uint32_t logn, const felt* gilo, const felt* gihi);
 
 // ---------------------------------------------------------------- hashing
 // leaves L (= n*B) of a coset-major LDE matrix (cols x B x n) -> nodes[L + i] (8 words each)
@@ -68,17 +67,40 @@ void launch_leaf_hash_fri(Prof& prof, hipStream_t s, const felt* E, uint64_t R, 
 // fused builders: leaves + all levels (nodes[1..2L)) in ceil(log2(L)/9) launches
 void launch_merkle_lde(Prof& prof, hipStream_t s, const felt* lde, uint32_t cols, uint32_t logB, uint64_t n,
                        uint32_t* nodes, uint64_t L);
-void launch_merkle_fri(Prof& prof, hipStream_t s, const felt* E, uint64_t R, uint32_t F, uint32_t* nodes);
+// FRI layer tree over coset-major evaluations (B cosets of 16*m16): leaf r = j + B*t'
+void launch_merkle_fri(Prof& prof, hipStream_t s, const felt* E, uint64_t m16, uint32_t logB, uint32_t F,
+                       uint32_t* nodes);
+// nodes[1..L) from leaf digests already in nodes[L..2L)
+void merkle_upper(Prof& prof, hipStream_t s, uint32_t* nodes, uint64_t L);
+// sharded commitments: hash the shard's rows (mode 0: LDE rows of cols columns;
+// mode 1: FRI rows of 16) into per-destination blocks; then, after the
+// all-to-all, rebuild the natural-order leaves of this rank's range and its subtree
+void launch_leaf_hash_shard(Prof& prof, hipStream_t s, int mode, const felt* src, uint64_t n, uint32_t cols,
+                            uint32_t logBl, uint32_t logrows, uint32_t logrr, uint32_t* send);
+void launch_merkle_from_shards(Prof& prof, hipStream_t s, const uint32_t* recv, uint32_t logB, uint32_t logrr,
+                               uint32_t* nodes);
 // internal nodes nodes[1..L) from leaves nodes[L..2L)
 void launch_merkle_tree(Prof& prof, hipStream_t s, uint32_t* nodes, uint64_t L);
 void launch_grind(Prof& prof, hipStream_t s, const uint32_t* seed_words_dev, uint64_t base, uint64_t count,
                   uint32_t bits, unsigned long long* result);
 
 // ---------------------------------------------------------------- constraints
+// Points of a coset-major shard: local index q = c*n + t is cx[c] * w_n^t,
+// cx[c] = g * w_N^(j of local coset c), twn = w_n^t for t < n/2 (the
+// stage-major twiddle level logn-1, read contiguously).
+struct PointMap {
+  const felt* cx;
+  const felt* twn;
+  uint32_t logn;
+};
+
+// The shard evaluates the CE cosets u in [u0, u0 + cel) (CE coset u lives in
+// LDE coset u * B/ce); its LDE matrices hold the cosets [j0, j0 + 2^logBl).
 struct EvalCommon {
   uint32_t logn, logB, logce, logN;
+  uint32_t u0, cel, j0, logBl;
   felt g, w_last;        // domain offset (3), w_n^(n-1)
-  const felt* tw;        // w_N^e
+  PointMap pm;           // x of the shard's CE points (cx per owned CE coset)
   const felt* zinv;      // ce entries: 1/(x^n - 1) on the CE domain (x^n = g^n * w_ce^s)
 };
 // MiMC: x' - (x + K)^7 ; boundary steps 0 and n-1 on column 0
@@ -102,9 +124,10 @@ struct LinearEvalArgs {
 void launch_eval_linear(Prof& prof, hipStream_t s, const EvalCommon& c, const LinearEvalArgs& a, const felt* lde,
                         felt* comp);
 
-// composition segment: A_h[p'] = src[p'*ce + rev(h)] * Gi[p'] * scale_h, h < C
-void launch_segment(Prof& prof, hipStream_t s, const felt* difout, uint32_t logn, uint32_t logce, uint32_t C,
-                    const felt* Gi, const felt* scales_dev, felt* out);
+// composition polynomial from CE-coset interpolations (see kernels.hip): for the
+// bit-reversed positions [p0, p0 + nR), n * c_m = sum_u Si_u * W_u * coefs[u][m]
+void launch_comp_dft(Prof& prof, hipStream_t s, const felt* recv, const uint32_t* blk, const felt* Si,
+                     const felt* coefs, uint32_t ce, uint32_t C, uint32_t logn, uint64_t p0, uint64_t nR, felt* out);
 
 // OOD evaluation of bit-reversed arrays (arrays contiguous, stride n) at x0 and x1
 // partial[(a * nblocks + b) * 2 + {0,1}] ; pw0/pw1 = x^(2^l) tables (logn entries, device)
@@ -114,18 +137,21 @@ void launch_eval_bitrev(Prof& prof, hipStream_t s, const felt* arrays, uint32_t 
 // DEEP composition over the LDE domain (natural order out)
 struct DeepArgs {
   uint32_t w, C, logB, logn, logN;
-  const felt* tlde;      // w x B x n
-  const felt* clde;      // C x B x n
+  uint32_t j0, logBl;    // shard cosets [j0, j0 + 2^logBl); output coset-major
+  const felt* tlde;      // w x Bl x n
+  const felt* clde;      // C x Bl x n
   const felt* gamma;     // w + C
   felt z, zg, kz, kzg, g;
-  const felt* tw;
+  PointMap pm;           // x of the shard's LDE points (cx per owned coset)
   felt* binv;            // scratch: one felt per 2048 LDE points
 };
 void launch_deep(Prof& prof, hipStream_t s, const DeepArgs& a, felt* out);
 
-// FRI fold-by-F (F = 16): out[r] = q_r(alpha), row r = [E[r + k*R]], x_r = off * w_D^r
-void launch_fri_fold(Prof& prof, hipStream_t s, const felt* E, uint64_t R, uint32_t F, felt alpha, felt off_inv,
-                     const felt* itw, uint32_t logN, uint32_t logD, const felt* eps_inv_dev, felt* out);
+// FRI fold-by-F (F = 16) over coset-major evaluations of the cosets [j0, j0+Bl)
+// (16*m16 positions each): natural row r = j + B*t', x_r = off * w_D^r
+void launch_fri_fold(Prof& prof, hipStream_t s, const felt* E, uint64_t m16, uint32_t Bl, uint32_t j0,
+                     uint32_t logB, uint32_t F, felt alpha, felt off_inv, const felt* itw, uint32_t logD,
+                     const felt* eps_inv_dev, felt* out);
 
 // gathers for query openings
 struct GatherSeg {
