@@ -7,10 +7,14 @@ MiMC AIR, n = 2^20, x0 = 42e6, ProofOptions(40, 8, 21,
 None, 16, 7, Algebraic, Algebraic). A "step" = one full proof (trace already
 resident in HBM -> serialized proof bytes on the host).
 
-Multi-GPU: one process per GPU (torchrun); each rank proves its own
-independent 2^20 trace on its own device ("replicas", weak scaling — no
-data-path collective). value = total proofs of all
-ranks / max-over-ranks wall time.
+Multi-GPU: one process per GPU (torchrun). Default `--mode replicas`: each
+rank proves its own independent 2^20 trace on its own device (weak scaling,
+no data-path collective). value = total proofs of all ranks / max-over-ranks
+wall time. `--mode sharded`: ONE proof per step split over all ranks by LDE
+coset (BASELINE configs[3] C4: MiMC 2^22; with --air agg configs[4] C5:
+GlobalUpdate 256 updates, 2^20 rows), collectives over the library's RCCL
+communicator (xGMI); strong scaling, value = proofs / wall time. See
+DESIGN.md §5.
 
 Also reported: `roofline` for the dominant kernel (algorithmic bytes per launch
 / HIP-event launch time on the prover's stream, live in the timed region) and
@@ -28,13 +32,38 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 
+# launch name (zkp_kernel_stats_table) -> kernel symbol in the rocprofv3 PMC
+# summaries that scripts/profile_round.sh writes (profiles/r01_pmc_traffic_*.json)
+KERNEL_SYMBOL = {
+    "ntt_dit": "void k_ntt8<true, 256>", "ntt_dif": "void k_ntt8<false, 256>", "deep": "k_deep",
+    "merkle_lde": "void k_merkle_lane<0, 3>", "eval_mimc": "k_eval_mimc", "eval_linear": "k_eval_linear",
+}
+
+
+def pmc_traffic(kernel: str, air: str, mode: str):
+    """HBM bytes per launch (FETCH_SIZE x2 + WRITE_SIZE, gfx950-corrected) of `kernel`
+    from the committed PMC summary of the same workload, or None."""
+    if mode != "replicas":
+        return None, None
+    name = {"mimc": "r01_pmc_traffic_mimc_c2.json", "agg": "r01_pmc_traffic_agg_c3.json"}[air]
+    path = os.path.join(ROOT, "profiles", name)
+    sym = KERNEL_SYMBOL.get(kernel)
+    if not sym or not os.path.exists(path):
+        return None, None
+    with open(path) as f:
+        rec = json.load(f).get(sym)
+    if not rec:
+        return None, None
+    return rec["traffic_per_launch"], f"profiles/{name} ({sym}, rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes)"
+
 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--log-n", type=int, default=20)
+    ap.add_argument("--log-n", type=int, default=None, help="trace length 2^k (default: the config's)")
+    ap.add_argument("--mode", choices=["replicas", "sharded"], default="replicas")
     ap.add_argument("--blowup", type=int, default=8)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-verify", action="store_true")
@@ -67,35 +96,49 @@ def main():
     from zk_stark_project_amd.helper import f64_to_felt
 
     ctx = _native.Context(local_rank)
+    sharded = args.mode == "sharded"
+    seed_rank = 0 if sharded else rank  # sharded: every rank holds the same trace
     if args.air == "mimc":
         air_id, width = AIR_MIMC, 1
-        n = 1 << args.log_n
+        log_n = args.log_n or (22 if sharded else 20)
+        n = 1 << log_n
         opts = ProofOptions(40, args.blowup, 21)  # (40, 8, 21, None, 16, 7, Algebraic, Algebraic)
         prover = MimcProver(opts, ctx)
-        trace = prover.build_trace(42 * 10**6 + rank, n)  # independent trace per rank
-        workload = f"MiMC AIR 2^{args.log_n}-step trace, blowup={args.blowup} (BASELINE configs[1])"
+        trace = prover.build_trace(42 * 10**6 + seed_rank, n)  # independent trace per replica
+        cfg = "BASELINE configs[3], domain-sharded" if sharded else "BASELINE configs[1]"
+        workload = f"MiMC AIR 2^{log_n}-step trace, blowup={args.blowup} ({cfg})"
     else:
         import random
         air_id, width = AIR_GLOBAL_UPDATE, 120
-        n = 1 << (18 if args.log_n == 20 else args.log_n)
+        log_n = args.log_n or (20 if sharded else 18)
+        n = 1 << log_n
         opts = ProofOptions.reference()  # (40, 16, 21, None, 16, 7, Algebraic, Algebraic)
-        rnd = random.Random(1 + rank)
+        rnd = random.Random(1 + seed_rank)
         r = lambda: rnd.randrange(2**64)
-        ndev = 64
+        ndev = 256 if sharded else 64
         prover = GlobalUpdateProver(opts, [[r() for _ in range(9)] for _ in range(6)], [r() for _ in range(6)],
                                     [[[r() for _ in range(9)] for _ in range(6)] for _ in range(ndev)],
                                     [[r() for _ in range(6)] for _ in range(ndev)], f64_to_felt(ndev),
                                     trace_length=n, blinding=[r() for _ in range(60)], ctx=ctx)
         trace = prover.build_trace()
-        workload = f"GlobalUpdate AIR, {ndev} updates padded to 2^{n.bit_length() - 1} rows, w=120 (BASELINE configs[2])"
+        cfg = "BASELINE configs[4], domain-sharded" if sharded else "BASELINE configs[2]"
+        workload = f"GlobalUpdate AIR, {ndev} updates padded to 2^{n.bit_length() - 1} rows, w=120 ({cfg})"
     pub = prover.get_pub_inputs(trace).to_elements()
     d_trace = ctx.alloc(trace.data.nbytes)
     ctx.to_device(d_trace, trace.data)
 
     from zk_stark_project_amd.replicas import aggregate_rate, timed_replicas
 
-    def prove_once():
-        return ctx.prove_device(air_id, d_trace, width, n, pub, opts)
+    comm = None
+    if sharded:
+        from zk_stark_project_amd.sharded import rccl_group_comm
+        comm = rccl_group_comm(ctx, rank, world) if world > 1 else _native.local_group(1)[0]
+
+        def prove_once():
+            return ctx.prove_sharded(comm, air_id, d_trace, pub, opts, shape=(width, n))
+    else:
+        def prove_once():
+            return ctx.prove_device(air_id, d_trace, width, n, pub, opts)
 
     verified = None
     if args.warmup > 0:
@@ -113,6 +156,8 @@ def main():
     ctx.set_profiling(False)
     stats = ctx.stats_table()
 
+    if comm is not None:
+        comm.close()
     if rank != 0:
         if dist is not None:
             dist.destroy_process_group()
@@ -125,6 +170,7 @@ def main():
     dom_avg_ms = dom["ms"] / dom["launches"]
     dom_bytes = dom["bytes"] / dom["launches"]
     achieved = dom_bytes / (dom_avg_ms * 1e-3) / 1e9
+    traffic, traffic_src = pmc_traffic(dom_name, args.air, args.mode)
     roofline = {
         "bound": "hbm",
         "kernel": dom_name,
@@ -132,14 +178,15 @@ def main():
         "peak": HBM_PEAK_GBS,
         "unit": "GB/s",
         "frac": round(achieved / HBM_PEAK_GBS, 4),
-        "traffic": None,
+        "traffic": traffic,
+        "traffic_source": traffic_src,
         "bytes_per_launch": dom_bytes,
         "avg_launch_ms": round(dom_avg_ms, 5),
         "share_of_device_time": round(dom["ms"] / total_ms, 3) if total_ms else None,
     }
 
     cpu = None
-    if world == 1 and not args.no_cpu_baseline:
+    if world == 1 and not args.no_cpu_baseline and not sharded:
         import oracle_ref
         tb = trace.to_bytes()
         pb = b"".join(v.to_bytes(16, "little") for v in pub)
@@ -157,25 +204,28 @@ def main():
         }
 
     ms = elapsed / args.steps * 1e3
-    metric = ("STARK proofs/sec + prove-time ms, MiMC AIR 2^20-step trace" if args.air == "mimc"
-              else "STARK proofs/sec + prove-time ms, aggregation AIR 2^18-step trace (C3)")
+    metric = (f"STARK proofs/sec + prove-time ms, MiMC AIR 2^{log_n}-step trace" if args.air == "mimc"
+              else f"STARK proofs/sec + prove-time ms, aggregation AIR 2^{log_n}-step trace")
+    if sharded:
+        metric += ", one proof domain-sharded over all GPUs"
     out = {
         "metric": metric,
-        "value": round(aggregate_rate(world, args.steps, elapsed), 3),
+        "value": round(aggregate_rate(1 if sharded else world, args.steps, elapsed), 3),
         "unit": "proofs/s",
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(ms, 3),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if sharded else "weak",
         "vs_baseline": None,
         "dtype": "f128 (u128 mod 2^128-45*2^40+1)",
         "data": "synthetic (MiMC trace x0=42e6+rank)" if args.air == "mimc" else "synthetic (seeded u64 model entries)",
         "config": {"workload": workload,
                    "trace_length": n, "trace_width": width, "blowup": opts.blowup_factor, "num_queries": 40,
                    "grinding": 21,
-                   "fri_folding": 16, "fri_remainder_max_degree": 7, "parallelism": f"replicas{world}"},
+                   "fri_folding": 16, "fri_remainder_max_degree": 7,
+                   "parallelism": f"coset-sharded{world} (RCCL)" if sharded else f"replicas{world}"},
         "roofline": roofline,
         "cpu_baseline": cpu,
         "proof_bytes": len(proof),

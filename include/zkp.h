@@ -153,6 +153,12 @@ int zkp_prove_sharded(zkp_ctx* ctx, zkp_comm* comm, zkp_air_id air, const zkp_fe
                       const zkp_proof_options* opts, uint8_t** proof, uint64_t* proof_len,
                       zkp_transcript* transcript /* nullable */);
 
+/* As zkp_prove_sharded with the full trace already in this rank's HBM. */
+int zkp_prove_sharded_device(zkp_ctx* ctx, zkp_comm* comm, zkp_air_id air, const void* d_trace_cols,
+                             uint32_t width, uint64_t n, const zkp_felt* pub_elems, uint64_t n_pub,
+                             const zkp_proof_options* opts, uint8_t** proof, uint64_t* proof_len,
+                             zkp_transcript* transcript /* nullable */);
+
 /* Device scratch helpers so callers (bench, tests) can keep traces in HBM. */
 int zkp_device_alloc(zkp_ctx* ctx, uint64_t bytes, void** d_ptr);
 int zkp_device_free(zkp_ctx* ctx, void* d_ptr);

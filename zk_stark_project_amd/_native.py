@@ -70,7 +70,7 @@ EXPORTED = [
     "zkp_copy_to_host", "zkp_trace_lde_commit", "zkp_merkle_commit_rows", "zkp_grind",
     "zkp_set_profiling", "zkp_kernel_stats", "zkp_reset_stats", "zkp_kernel_stats_table",
     "zkp_build_mimc_trace", "zkp_prove_sharded", "zkp_comm_local_group", "zkp_comm_rccl_unique_id",
-    "zkp_comm_rccl_create", "zkp_comm_destroy", "zkp_comm_rank", "zkp_comm_world",
+    "zkp_comm_rccl_create", "zkp_comm_destroy", "zkp_comm_rank", "zkp_comm_world", "zkp_prove_sharded_device",
 ]
 
 _lib = None
@@ -115,8 +115,9 @@ def load():
         L.zkp_kernel_stats_table.argtypes = [vp, ctypes.POINTER(ctypes.c_char_p)]
         L.zkp_build_mimc_trace.argtypes = [ctypes.c_char_p, u64, vp]
         L.zkp_build_mimc_trace.restype = i32
-        L.zkp_prove_sharded.argtypes = [vp, vp, i32, vp, u32, u64, vp, u64, popt, ctypes.POINTER(pu8),
-                                        ctypes.POINTER(u64), ctypes.POINTER(Transcript)]
+        for name in ("zkp_prove_sharded", "zkp_prove_sharded_device"):
+            getattr(L, name).argtypes = [vp, vp, i32, vp, u32, u64, vp, u64, popt, ctypes.POINTER(pu8),
+                                         ctypes.POINTER(u64), ctypes.POINTER(Transcript)]
         L.zkp_comm_local_group.argtypes = [i32, ctypes.POINTER(vp)]
         L.zkp_comm_rccl_unique_id.argtypes = [ctypes.c_char_p]
         L.zkp_comm_rccl_create.argtypes = [vp, ctypes.c_char_p, i32, i32, ctypes.POINTER(vp)]
@@ -239,17 +240,25 @@ class Context:
         self.lib.zkp_free(out)
         return data, tr
 
-    def prove_sharded(self, comm: "Comm", air_id: int, trace: np.ndarray, pub, options: ProofOptions):
-        """One rank of a coset-sharded proof (collective over `comm`)."""
-        w, n = int(trace.shape[0]), int(trace.shape[1])
+    def prove_sharded(self, comm: "Comm", air_id: int, trace, pub, options: ProofOptions, shape=None):
+        """One rank of a coset-sharded proof (collective over `comm`). `trace` is a
+        (width, n, 2) uint64 host array, or a device pointer with shape=(width, n)."""
         pubb = b"".join(int(v).to_bytes(16, "little") for v in pub)
         out = ctypes.POINTER(ctypes.c_uint8)()
         olen = ctypes.c_uint64()
         tr = Transcript()
         oc = options.to_c()
-        trace = np.ascontiguousarray(trace, dtype=np.uint64)
-        rc = self.lib.zkp_prove_sharded(self.ptr, comm.ptr, air_id, trace.ctypes.data, w, n, pubb, len(pub),
-                                        ctypes.byref(oc), ctypes.byref(out), ctypes.byref(olen), ctypes.byref(tr))
+        if shape is None:
+            w, n = int(trace.shape[0]), int(trace.shape[1])
+            trace = np.ascontiguousarray(trace, dtype=np.uint64)
+            rc = self.lib.zkp_prove_sharded(self.ptr, comm.ptr, air_id, trace.ctypes.data, w, n, pubb, len(pub),
+                                            ctypes.byref(oc), ctypes.byref(out), ctypes.byref(olen),
+                                            ctypes.byref(tr))
+        else:
+            w, n = shape
+            rc = self.lib.zkp_prove_sharded_device(self.ptr, comm.ptr, air_id, trace, w, n, pubb, len(pub),
+                                                   ctypes.byref(oc), ctypes.byref(out), ctypes.byref(olen),
+                                                   ctypes.byref(tr))
         self._check(rc, f"zkp_prove_sharded(rank {comm.rank}/{comm.world})")
         data = ctypes.string_at(out, olen.value)
         self.lib.zkp_free(out)

@@ -1273,6 +1273,20 @@ int zkp_prove_sharded(zkp_ctx* ctx, zkp_comm* comm, zkp_air_id air, const zkp_fe
   return rc;
 }
 
+int zkp_prove_sharded_device(zkp_ctx* ctx, zkp_comm* comm, zkp_air_id air, const void* d_trace, uint32_t width,
+                             uint64_t n, const zkp_felt* pub, uint64_t n_pub, const zkp_proof_options* opts,
+                             uint8_t** proof, uint64_t* proof_len, zkp_transcript* transcript) {
+  int rc = guarded(ctx, [&] {
+    ctx->err.clear();
+    HIP_CHECK(hipSetDevice(ctx->device));
+    if (!d_trace || !comm) return (int)ZKP_ERR_ARGUMENT;
+    return prove_impl(ctx, comm, air, (const felt*)d_trace, width, n, pub, n_pub, opts, proof, proof_len,
+                      transcript);
+  });
+  if (rc && comm) comm->abort();
+  return rc;
+}
+
 int zkp_comm_local_group(int world, zkp_comm** comms) {
   if (!comms || world < 1 || world > 64) return ZKP_ERR_ARGUMENT;
   try {
