@@ -47,7 +47,9 @@ typedef struct zkp_felt {
  *                  width 1, pub = [x0, x_last].
  *  GLOBAL_UPDATE : GlobalUpdateAir, src/aggregation/air.rs:89-151. width 120,
  *                  pub = GlobalUpdateInputs::to_elements() (123 felts, air.rs:57-81).
- *  TRAINING_UPDATE: reserved; returns ZKP_ERR_UNSUPPORTED_AIR. */
+ *  TRAINING_UPDATE: TrainingUpdateAir, src/training/air.rs:101-292. width 240,
+ *                  pub = TrainingUpdateInputs::to_elements() (air.rs:74-98: 244 + bs*(FE+AC)
+ *                  felts); transitions identically zero (current_step() == 0). */
 typedef enum zkp_air_id {
   ZKP_AIR_MIMC = 1,
   ZKP_AIR_GLOBAL_UPDATE = 2,

@@ -135,3 +135,20 @@ def test_global_update_c5_size_single_gpu(ctx):
     bad = list(pub_el)
     bad[60] = (bad[60] + 1) % P
     assert O.verify(AIR_GLOBAL_UPDATE, gpu, to_bytes(bad), opts) != 0
+
+
+@pytest.mark.parametrize("bs,blowup,grind", [(0, 16, 4), (1, 16, 8), (2, 8, 0), (4, 16, 21), (17, 16, 16)])
+def test_training_update_proof_bit_exact(ctx, bs, blowup, grind):
+    from test_training import tu_prover
+    from zk_stark_project_amd import AIR_TRAINING_UPDATE
+    opts = ProofOptions(40, blowup, grind)
+    p = tu_prover(bs, seed=100 + bs, options=opts)
+    tr = p.build_trace()
+    pub_el = p.get_pub_inputs(tr).to_elements()
+    pub = to_bytes(pub_el)
+    gpu, gtr = ctx.prove(AIR_TRAINING_UPDATE, tr.data, pub_el, opts)
+    ref, otr = O.prove(AIR_TRAINING_UPDATE, tr.to_bytes(), 240, tr.length(), pub, opts)
+    assert bytes(gtr.trace_root) == bytes(otr.trace_root)
+    assert bytes(gtr.constraint_root) == bytes(otr.constraint_root)
+    assert gpu == ref
+    assert O.verify(AIR_TRAINING_UPDATE, gpu, pub, opts) == 0

@@ -91,3 +91,16 @@ def test_mimc_sharded_2_20_world8(ctx, rank_ctxs):
     ref, _ = ctx.prove(AIR_MIMC, trace.data, pub, opts)
     res = prove_local_group(8, AIR_MIMC, trace.data, pub, opts, contexts=rank_ctxs[:8])
     check_all_equal(res, ref)
+
+
+@pytest.mark.parametrize("world", [2, 8])
+def test_training_update_sharded_equals_single(ctx, rank_ctxs, world):
+    from test_training import tu_prover
+    from zk_stark_project_amd import AIR_TRAINING_UPDATE
+    opts = ProofOptions.reference()
+    p = tu_prover(20, seed=world, options=opts)  # n = 4096
+    tr = p.build_trace()
+    pub = p.get_pub_inputs(tr).to_elements()
+    ref, _ = ctx.prove(AIR_TRAINING_UPDATE, tr.data, pub, opts)
+    res = prove_local_group(world, AIR_TRAINING_UPDATE, tr.data, pub, opts, contexts=rank_ctxs[:world])
+    check_all_equal(res, ref)

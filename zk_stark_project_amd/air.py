@@ -112,3 +112,63 @@ class GlobalUpdateAir:
         out = [Assertion(i, last, final[i]) for i in range(D_STATE)]
         out += [Assertion(i, last, 0) for i in range(D_STATE, 2 * D_STATE)]
         return out
+
+
+# ------------------------------------------------------------------ training
+TU_STATE = 2 * (AC * FE + AC)   # 120: flattened [v, s] pairs (src/training/prover.rs:98-103)
+TU_WIDTH = 2 * TU_STATE         # 240: masked state || masks
+
+
+@dataclass
+class TrainingUpdateInputs:
+    """src/training/air.rs:18-99."""
+    initial_masked: list
+    final_masked: list
+    steps: int
+    x_batch: list        # BS x FE
+    y_batch: list        # BS x AC
+    learning_rate: int
+    precision: int
+    batch_size: int
+
+    def to_elements(self):
+        """air.rs:74-98: initial || final || f64(steps) || f64(bs) || x || y || lr || precision."""
+        from .helper import f64_to_felt
+        e = list(self.initial_masked) + list(self.final_masked)
+        e.append(f64_to_felt(float(self.steps)))
+        e.append(f64_to_felt(float(self.batch_size)))
+        for row in self.x_batch:
+            e.extend(row)
+        for row in self.y_batch:
+            e.extend(row)
+        e.append(self.learning_rate)
+        e.append(self.precision)
+        return e
+
+    def to_bytes(self) -> bytes:
+        """`Serializable::write_into` (air.rs:38-70): the same elements, 16 B LE each."""
+        return b"".join(int(v).to_bytes(16, "little") for v in self.to_elements())
+
+
+class TrainingUpdateAir:
+    """src/training/air.rs:101-292: width 240, 240 degree-1 transition constraints
+    that evaluate to zero (current_step() == 0), masked state asserted
+    at row 0 and row trace_length - 1 (240 assertions)."""
+    AIR_ID = AIR_TRAINING_UPDATE
+    WIDTH = TU_WIDTH
+    TRANSITION_DEGREE = 1
+    CYCLE = 0
+
+    def __init__(self, trace_length: int, pub_inputs: TrainingUpdateInputs, options):
+        if len(pub_inputs.x_batch) != pub_inputs.batch_size or len(pub_inputs.y_batch) != pub_inputs.batch_size:
+            raise ValueError("batch data does not match batch_size in public inputs")  # air.rs:120-123
+        self.trace_length = trace_length
+        self.pub_inputs = pub_inputs
+        self.options = options
+
+    def get_assertions(self):
+        half = self.WIDTH // 2
+        last = self.trace_length - 1
+        out = [Assertion(i, 0, self.pub_inputs.initial_masked[i]) for i in range(half)]
+        out += [Assertion(i, last, self.pub_inputs.final_masked[i]) for i in range(half)]
+        return out

@@ -727,11 +727,17 @@ __global__ __launch_bounds__(TPB) void k_eval_mimc(EvalCommon c, MimcEvalArgs a,
   });
 }
 
+// Linear AIRs. TRANS: transition sum_c a_c*next_c + b_c*cur_c divided by Z_T
+// (GlobalUpdate); without it the transition part is identically zero
+// (TrainingUpdate). Boundary: group 0 = sum_c beta0_c*cur_c - bconst0
+// over (x - w_b0); TWO adds group 1 = sum_c beta1_c*cur_c - bconst1 over (x - w_b1).
+template <bool TRANS, bool TWO>
 __global__ __launch_bounds__(TPB) void k_eval_linear(EvalCommon c, LinearEvalArgs a, const felt* __restrict__ lde,
                                                      const felt* __restrict__ binv, felt* __restrict__ comp) {
   __shared__ felt s_pre[TPB], s_suf[TPB];
   const uint64_t M = (uint64_t)c.cel << c.logn;
   const uint64_t cstride = 1ull << (c.logn + c.logBl);
+  const uint32_t W = a.width;
   felt tpart[EVAL_CH], bnum[EVAL_CH], den[EVAL_CH];
   static_for<0, EVAL_CH>([&](auto k) {
     const uint64_t q0 = EVAL_POINT(k);
@@ -740,16 +746,23 @@ __global__ __launch_bounds__(TPB) void k_eval_linear(EvalCommon c, LinearEvalArg
     const CePoint pt = ce_point(c, q);
     const felt* pc = lde + pt.off;
     const felt* pn = lde + pt.off_next;
-    felt tr = zero(), bs = zero();
-    for (uint32_t col = 0; col < a.width; col++) {
-      felt cur = pc[col * cstride], nxt = pn[col * cstride];
-      tr = add(tr, add(mul(a.coefs[col], nxt), mul(a.coefs[a.width + col], cur)));
-      bs = add(bs, mul(a.coefs[2 * a.width + col], cur));
+    felt tr = zero(), bs0 = zero(), bs1 = zero();
+    for (uint32_t col = 0; col < W; col++) {
+      felt cur = pc[col * cstride];
+      if (TRANS) tr = add(tr, add(mul(a.coefs[col], pn[col * cstride]), mul(a.coefs[W + col], cur)));
+      bs0 = add(bs0, mul(a.coefs[2 * W + col], cur));
+      if (TWO) bs1 = add(bs1, mul(a.coefs[3 * W + col], cur));
     }
     felt x = point_x(c.pm, q);
-    tpart[k] = mul(mul(tr, sub(x, c.w_last)), c.zinv[pt.u]);
-    bnum[k] = sub(bs, a.bconst);
-    den[k] = valid ? sub(x, a.w_bstep) : one();
+    tpart[k] = TRANS ? mul(mul(tr, sub(x, c.w_last)), c.zinv[pt.u]) : zero();
+    if (TWO) {
+      felt e0 = sub(x, a.w_bstep), e1 = sub(x, a.w_bstep1);
+      bnum[k] = add(mul(sub(bs0, a.bconst), e1), mul(sub(bs1, a.bconst1), e0));
+      den[k] = valid ? mul(e0, e1) : one();
+    } else {
+      bnum[k] = sub(bs0, a.bconst);
+      den[k] = valid ? sub(x, a.w_bstep) : one();
+    }
   });
   block_batch_inverse(den, s_pre, s_suf, binv[blockIdx.x]);
   static_for<0, EVAL_CH>([&](auto k) {
@@ -1246,10 +1259,19 @@ void launch_eval_mimc(Prof& prof, hipStream_t s, const EvalCommon& c, const Mimc
 void launch_eval_linear(Prof& prof, hipStream_t s, const EvalCommon& c, const LinearEvalArgs& a, const felt* lde,
                         felt* comp) {
   uint64_t M = (uint64_t)c.cel << c.logn;
-  if (!a.binv_ready) launch_den_inverse(prof, s, c.pm, M, a.w_bstep, zero(), 0, a.binv);
-  LAUNCH(prof, "eval_linear", s, (double)M * (a.width * 16.0 + 16.0),
-         hipLaunchKernelGGL(k_eval_linear, dim3(blocks_for((M + EVAL_CH - 1) / EVAL_CH)), dim3(TPB), 0, s, c, a, lde,
-                            a.binv, comp));
+  const bool two = a.two_groups;
+  if (!a.binv_ready) launch_den_inverse(prof, s, c.pm, M, a.w_bstep, a.w_bstep1, two ? 1 : 0, a.binv);
+  dim3 g(blocks_for((M + EVAL_CH - 1) / EVAL_CH));
+  const double bytes = (double)M * (a.width * (a.transition ? 32.0 : 16.0) + 16.0);
+  if (a.transition && !two)
+    LAUNCH(prof, "eval_linear", s, bytes,
+           hipLaunchKernelGGL((k_eval_linear<true, false>), g, dim3(TPB), 0, s, c, a, lde, a.binv, comp));
+  else if (!a.transition && two)
+    LAUNCH(prof, "eval_linear", s, bytes,
+           hipLaunchKernelGGL((k_eval_linear<false, true>), g, dim3(TPB), 0, s, c, a, lde, a.binv, comp));
+  else
+    LAUNCH(prof, "eval_linear", s, bytes,
+           hipLaunchKernelGGL((k_eval_linear<true, true>), g, dim3(TPB), 0, s, c, a, lde, a.binv, comp));
 }
 
 void launch_eval_bitrev(Prof& prof, hipStream_t s, const felt* arrays, uint32_t narrays, uint32_t logn,

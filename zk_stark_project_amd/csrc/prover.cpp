@@ -183,6 +183,8 @@ struct Writer {
 
 // ------------------------------------------------------------------ AIR metadata
 constexpr uint32_t GU_D = 60;  // AC*FE + AC (src/helper.rs:18-20)
+constexpr uint32_t TU_W = 240;  // 4*(AC*FE + AC), src/training/prover.rs:98-103
+constexpr uint32_t TU_AC = 6, TU_FE = 9;
 
 struct AirDesc {
   int id;
@@ -233,6 +235,27 @@ int build_air(AirDesc& a, int id, uint32_t w, uint64_t n, const std::vector<felt
       a.a_col.push_back(i);
       a.a_step.push_back(steps - 1);
       a.a_val.push_back(i < GU_D ? pub[60 + i] : zero());
+    }
+    return 0;
+  }
+  if (id == ZKP_AIR_TRAINING_UPDATE) {
+    // src/training/air.rs:101-151; public inputs (to_elements :74-98): initial (w/2) || final (w/2) ||
+    // f64(steps) || f64(bs) || x_batch (bs*FE) || y_batch (bs*AC) || lr || precision
+    if (w != TU_W || pub.size() < TU_W + 4) return ZKP_ERR_PUB_INPUTS;
+    felt bsf = pub[TU_W + 1];
+    if (bsf.hi != 0 || bsf.lo % 1000000ull) return ZKP_ERR_PUB_INPUTS;
+    uint64_t bs = bsf.lo / 1000000ull;
+    if (pub.size() != (uint64_t)TU_W + 4 + bs * (TU_FE + TU_AC)) return ZKP_ERR_PUB_INPUTS;
+    const uint32_t half = TU_W / 2;
+    a.num_t = TU_W;  // all degree 1, all identically zero (current_step() == 0)
+    a.base_degree = 1;
+    a.cycle = 0;
+    a.a_col.resize(2 * half);
+    a.a_step.resize(2 * half);
+    a.a_val.resize(2 * half);
+    for (uint32_t i = 0; i < half; i++) {  // air.rs:140-147
+      a.a_col[i] = i; a.a_step[i] = 0; a.a_val[i] = pub[i];
+      a.a_col[half + i] = i; a.a_step[half + i] = n - 1; a.a_val[half + i] = pub[half + i];
     }
     return 0;
   }
@@ -754,9 +777,9 @@ int prove_impl(zkp_ctx* ctx, zkp_comm* cm, int air_id, const felt* d_trace, uint
       ma.binv_ready = ctx->have_cached(key);
       ma.binv = ctx->buf<felt>(key, ((uint64_t)cel * n) / 2048 + 1);
       launch_eval_mimc(pf, st, ec, ma, tlde, comp);
-    } else {
+    } else if (air.id == ZKP_AIR_GLOBAL_UPDATE) {
       // GlobalUpdate: T = sum_i a^i (k*next_i - k*cur_i - next_{i+60}); B = sum_c b_c (cur_c - v_c)
-      std::vector<felt> co(3 * w, zero());
+      std::vector<felt> co(4 * w, zero());
       for (uint32_t i = 0; i < GU_D; i++) {
         co[i] = mul(cc[i], air.k);                    // next_i
         co[w + i] = neg(mul(cc[i], air.k));           // cur_i
@@ -771,10 +794,41 @@ int prove_impl(zkp_ctx* ctx, zkp_comm* cm, int air_id, const felt* d_trace, uint
       ctx->upload(dco, co.data(), co.size() * 16);
       LinearEvalArgs la;
       la.width = w;
+      la.transition = true;
+      la.two_groups = false;
       la.coefs = dco;
       la.bconst = bconst;
       la.w_bstep = pow_u64(wn, air.a_step[0]);
+      la.bconst1 = zero();
+      la.w_bstep1 = zero();
       std::string key = "binv_lin_" + dom + "_" + std::to_string(air.a_step[0]);
+      la.binv_ready = ctx->have_cached(key);
+      la.binv = ctx->buf<felt>(key, ((uint64_t)cel * n) / 2048 + 1);
+      launch_eval_linear(pf, st, ec, la, tlde, comp);
+    } else {
+      // TrainingUpdate: transitions identically zero; boundary groups at rows 0 and n-1 over
+      // the masked columns 0..w/2 (the mask columns are never read)
+      const uint32_t half = w / 2;
+      std::vector<felt> co(4 * half, zero());
+      felt bc0 = zero(), bc1 = zero();
+      for (uint32_t i = 0; i < half; i++) {
+        co[2 * half + i] = cc[air.num_t + i];
+        co[3 * half + i] = cc[air.num_t + half + i];
+        bc0 = add(bc0, mul(cc[air.num_t + i], air.a_val[i]));
+        bc1 = add(bc1, mul(cc[air.num_t + half + i], air.a_val[half + i]));
+      }
+      felt* dco = ctx->buf<felt>("lin_coefs", co.size());
+      ctx->upload(dco, co.data(), co.size() * 16);
+      LinearEvalArgs la;
+      la.width = half;
+      la.transition = false;
+      la.two_groups = true;
+      la.coefs = dco;
+      la.bconst = bc0;
+      la.w_bstep = one();
+      la.bconst1 = bc1;
+      la.w_bstep1 = ec.w_last;
+      std::string key = "binv_tu_" + dom;
       la.binv_ready = ctx->have_cached(key);
       la.binv = ctx->buf<felt>(key, ((uint64_t)cel * n) / 2048 + 1);
       launch_eval_linear(pf, st, ec, la, tlde, comp);

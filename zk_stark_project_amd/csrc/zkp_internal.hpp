@@ -112,12 +112,16 @@ struct MimcEvalArgs {
 };
 void launch_eval_mimc(Prof& prof, hipStream_t s, const EvalCommon& c, const MimcEvalArgs& a, const felt* lde,
                       felt* comp);
-// linear AIR: T = sum_c a_c*next_c + b_c*cur_c ; one boundary group at step `bstep`:
-// B = sum_c beta_c*cur_c - bconst ; divisor (x - w^bstep)
+// linear AIRs (GlobalUpdate, TrainingUpdate): optional transition
+// T = sum_c a_c*next_c + b_c*cur_c over Z_T; boundary group 0 at step b0
+// (sum_c beta0_c*cur_c - bconst over x - w^b0) and optional group 1 at step b1.
+// coefs = [a (width) | b (width) | beta0 (width) | beta1 (width)], width = columns read
 struct LinearEvalArgs {
   uint32_t width;
-  const felt* coefs;     // 3*width: a_c, b_c, beta_c
+  bool transition, two_groups;
+  const felt* coefs;
   felt bconst, w_bstep;
+  felt bconst1, w_bstep1;
   felt* binv;            // one felt per 2048 CE points
   bool binv_ready;
 };

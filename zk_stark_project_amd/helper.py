@@ -70,3 +70,141 @@ def mimc_hash_matrix(w, b, round_constants) -> int:
             z = mimc_cipher(w[i][j], round_constants[j % n], z)
         z = mimc_cipher(b[i], round_constants[i % n], z)
     return z
+
+
+# --------------------------------------------------------------------------
+# signed fixed-point arithmetic over the field (src/signed.rs), used by the
+# training trace builder. Semantics are reproduced exactly, including
+# sub_generic(a, 0, b, 0) returns a + b.
+SIGNED_MAX = felt_new(MAX)  # signed.rs:3 Felt::new(u128::MAX)
+
+
+def _cleanse(v: int, s: int) -> int:
+    """signed.rs:11-14."""
+    return ((1 - s) * v + s * (SIGNED_MAX - v + 1)) % P
+
+
+def add_generic(a: int, s_a: int, b: int, s_b: int) -> tuple[int, int]:
+    """signed.rs:16-25."""
+    a_c, b_c = _cleanse(a, s_a), _cleanse(b, s_b)
+    ind = s_a * s_b % P
+    c = (ind * (SIGNED_MAX + 1 - a_c - b_c) + (1 - ind) * (a + b)) % P
+    return c, ind
+
+
+def sub_generic(a: int, s_a: int, b: int, s_b: int) -> tuple[int, int]:
+    """signed.rs:27-30 — a + (-b), with the reference's sign handling."""
+    return add_generic(a, s_a, b, (1 - s_b) % P)
+
+
+def mul_generic(a: int, s_a: int, b: int, s_b: int) -> tuple[int, int]:
+    """signed.rs:32-39."""
+    prod = _cleanse(a, s_a) * _cleanse(b, s_b) % P
+    sign = (s_a + s_b - s_a * s_b * 2) % P
+    return (sign * (SIGNED_MAX - prod + 1) + (1 - sign) * prod) % P, sign
+
+
+def div_generic(a: int, s_a: int, b: int, s_b: int) -> tuple[int, int]:
+    """signed.rs:41-48 (field inverse; inv(0) = 0)."""
+    from .field import inv
+    q = _cleanse(a, s_a) * inv(_cleanse(b, s_b)) % P
+    sign = (s_a + s_b - s_a * s_b * 2) % P
+    return (sign * (SIGNED_MAX + 1 - q) + (1 - sign) * q) % P, sign
+
+
+# felt-only wrappers (signed.rs:53-64), re-exported by helper.rs:3 as
+# add / subtract / multiply / divide with argument order (a, b, s_a, s_b)
+def add(a, b, s_a, s_b):
+    return add_generic(a, s_a, b, s_b)
+
+
+def subtract(a, b, s_a, s_b):
+    return sub_generic(a, s_a, b, s_b)
+
+
+def multiply(a, b, s_a, s_b):
+    return mul_generic(a, s_a, b, s_b)
+
+
+def divide(a, b, s_a, s_b):
+    return div_generic(a, s_a, b, s_b)
+
+
+def _rust_round_i128(y: float) -> int:
+    """`(y).round() as i128`: half away from zero; NaN -> 0; saturating."""
+    if y != y:
+        return 0
+    if math.isinf(y) or abs(y) >= 2.0**127:
+        return (1 << 127) - 1 if y > 0 else -(1 << 127)
+    r = math.floor(abs(y))
+    if abs(y) - r >= 0.5:
+        r += 1
+    return r if y >= 0 else -r
+
+
+def f64_to_signed_felt(x: float, scale: float) -> tuple[int, int]:
+    """helper.rs:48-51."""
+    return encode_signed(_rust_round_i128(x * scale))
+
+
+def label_to_one_hot(label: float, ac: int, precision: float):
+    """helper.rs:150-162."""
+    v, s = [0] * ac, [0] * ac
+    idx = 0 if label < 1.0 else max(int(label) - 1, 0)
+    if idx < ac:
+        v[idx], s[idx] = f64_to_signed_felt(precision, 1.0)
+    return v, s
+
+
+def split_state_with_sign(row, ac: int, fe: int):
+    """helper.rs:165-195 — [v0,s0,v1,s1,...] -> (w, b, w_sign, b_sign)."""
+    assert len(row) == 2 * ac * (fe + 1), "split_state_with_sign: bad row length"
+    w = [[row[2 * (j * fe + i)] for i in range(fe)] for j in range(ac)]
+    ws = [[row[2 * (j * fe + i) + 1] for i in range(fe)] for j in range(ac)]
+    b = [row[2 * (ac * fe + j)] for j in range(ac)]
+    bs = [row[2 * (ac * fe + j) + 1] for j in range(ac)]
+    return w, b, ws, bs
+
+
+def mse_prime(y_true, y_pred, y_pred_sign, pr):
+    """helper.rs:245-269."""
+    ac = len(y_true)
+    ac_f = f64_to_felt(float(ac))
+    res, res_s = [0] * ac, [0] * ac
+    for i in range(ac):
+        t, ts = subtract(y_pred[i], y_true[i], y_pred_sign[i], 0)
+        t2, t2s = multiply(t, f64_to_felt(2.0), ts, 0)
+        res[i], res_s[i] = divide(t2, ac_f, t2s, 0)
+    return res, res_s
+
+
+def forward_propagation_layer(w, b, x, w_sign, b_sign, x_sign, pr):
+    """helper.rs:282-330."""
+    ac, fe = len(b), len(x)
+    wx, wxs = [0] * ac, [0] * ac
+    for j in range(ac):
+        t, ts = 0, 0
+        for i in range(fe):
+            ti, tis = multiply(w[j][i], x[i], w_sign[j][i], x_sign[i])
+            t, ts = add(t, ti, ts, tis)
+        wx[j], wxs[j] = divide(t, pr, ts, 0)
+    out, out_s = [0] * ac, [0] * ac
+    for j in range(ac):
+        out[j], out_s[j] = add(wx[j], b[j], wxs[j], b_sign[j])
+    return out, out_s
+
+
+def backward_propagation_layer(w, b, x, output_error, learning_rate, pr, w_sign, b_sign, x_sign,
+                               output_error_sign):
+    """helper.rs:345-400 (updates in place and returns copies, like the reference)."""
+    ac, fe = len(b), len(x)
+    for i in range(ac):
+        t, ts = divide(output_error[i], learning_rate, output_error_sign[i], 0)
+        b[i], b_sign[i] = subtract(b[i], t, b_sign[i], ts)
+    for j in range(fe):
+        for i in range(ac):
+            prod, ps = multiply(output_error[i], x[j], output_error_sign[i], x_sign[j])
+            t, ts = divide(prod, learning_rate, ps, 0)
+            grad, gs = divide(t, pr, ts, 0)
+            w[i][j], w_sign[i][j] = subtract(w[i][j], grad, w_sign[i][j], gs)
+    return [r[:] for r in w], b[:], [r[:] for r in w_sign], b_sign[:]

@@ -1,6 +1,7 @@
 """Host-side mirror of the reference's `Prover` plug-ins.
 
 `GlobalUpdateProver` follows /root/reference/src/aggregation/prover.rs:15-249
+and `TrainingUpdateProver` /root/reference/src/training/prover.rs:18-301
 (same constructor arguments, trace construction and public inputs);
 `MimcProver` is the prover for the builder-defined MiMC AIR (SURVEY.md
 Appendix B). `prove(trace)` hands the trace to libzkp.so (HIP, gfx950) through
@@ -13,10 +14,11 @@ import secrets
 import numpy as np
 
 from . import _native
-from .air import (AIR_GLOBAL_UPDATE, AIR_MIMC, D_STATE, GlobalUpdateAir, GlobalUpdateInputs,
-                  MimcAir, MimcInputs)
+from .air import (AIR_GLOBAL_UPDATE, AIR_MIMC, D_STATE, TU_STATE, GlobalUpdateAir, GlobalUpdateInputs,
+                  MimcAir, MimcInputs, TrainingUpdateAir, TrainingUpdateInputs)
 from .field import P, inv, pack, unpack
-from .helper import AC, FE, get_round_constants, mimc_hash_matrix
+from .helper import (AC, FE, backward_propagation_layer, forward_propagation_layer, get_round_constants,
+                     mimc_hash_matrix, mse_prime, split_state_with_sign)
 from .options import ProofOptions
 
 
@@ -183,3 +185,83 @@ class GlobalUpdateProver(Prover):
         digest = mimc_hash_matrix(new_w, new_b, get_round_constants())
         return GlobalUpdateInputs(self.masked_global_w, self.masked_global_b, new_w, new_b,
                                   self.k, digest, steps)
+
+
+# ------------------------------------------------------------------ training
+class TrainingUpdateProver(Prover):
+    """src/training/prover.rs:18-301 — masked trace of `batch_size` SGD steps.
+
+    The reference samples its masks with `thread_rng` (prover.rs:117-126,
+    188-196); here they come from `mask_seed` (random when None) so a trace can
+    be rebuilt for parity tests."""
+
+    AIR = TrainingUpdateAir
+
+    def __init__(self, options, initial_w, initial_b, w_sign, b_sign, x_batch, x_batch_sign, y_batch,
+                 learning_rate, precision, batch_size, mask_seed=None, ctx=None):
+        super().__init__(options, ctx)
+        if not (len(x_batch) == len(x_batch_sign) == len(y_batch) == batch_size):
+            raise ValueError("batch data does not match batch_size")  # prover.rs:57-59
+        ac, fe = len(initial_b), len(initial_w[0])
+        state_cells = ac * fe + ac
+        self.initial_w, self.initial_b = initial_w, initial_b
+        self.w_sign, self.b_sign = w_sign, b_sign
+        self.x_batch, self.x_batch_sign, self.y_batch = x_batch, x_batch_sign, y_batch
+        self.learning_rate, self.precision = learning_rate % P, precision % P
+        self.batch_size = batch_size
+        self.trace_length = max(1 << (2 * state_cells * batch_size - 1).bit_length(), 16)  # prover.rs:63
+        self.mask_seed = secrets.randbits(63) if mask_seed is None else mask_seed
+        self._raw_rows = None
+
+    def _raw_states(self):
+        """The unmasked flattened state [v0,s0,v1,s1,...] after each processed sample."""
+        if self._raw_rows is None:
+            ac, fe = len(self.initial_b), len(self.initial_w[0])
+            raw = []
+            for row, srow in zip(self.initial_w, self.w_sign):
+                for v, s in zip(row, srow):
+                    raw += [v % P, s % P]
+            for v, s in zip(self.initial_b, self.b_sign):
+                raw += [v % P, s % P]
+            states = [raw]
+            for step in range(1, self.batch_size + 1):  # prover.rs:139-181
+                w, b, ws, bs = split_state_with_sign(raw, ac, fe)
+                k = step - 1
+                out, out_s = forward_propagation_layer(w, b, self.x_batch[k], ws, bs, self.x_batch_sign[k],
+                                                       self.precision)
+                err, err_s = mse_prime(self.y_batch[k], out, out_s, self.precision)
+                w2, b2, w2s, b2s = backward_propagation_layer(w, b, self.x_batch[k], err, self.learning_rate,
+                                                              self.precision, ws, bs, self.x_batch_sign[k],
+                                                              err_s)
+                raw = []
+                for rv, sv in zip(w2, w2s):
+                    for v, s in zip(rv, sv):
+                        raw += [v, s]
+                for v, s in zip(b2, b2s):
+                    raw += [v, s]
+                states.append(raw)
+            self._raw_rows = states
+        return self._raw_rows
+
+    def build_trace(self) -> TraceTable:
+        """prover.rs:90-218: row t = [raw_t + mask_t || mask_t]; raw stops changing after batch_size."""
+        n, half = self.trace_length, TU_STATE
+        states = self._raw_states()
+        rng = np.random.default_rng(self.mask_seed)
+        masks = rng.integers(0, 1 << 64, size=(n, half), dtype=np.uint64, endpoint=False)
+        cols = np.zeros((2 * half, n, 2), dtype=np.uint64)
+        cols[half:, :, 0] = masks.T
+        for t in range(n):
+            raw = states[min(t, len(states) - 1)]
+            mrow = masks[t].tolist()
+            cols[:half, t] = pack([(r + m) % P for r, m in zip(raw, mrow)])
+        return TraceTable(cols)
+
+    def get_pub_inputs(self, trace: TraceTable) -> TrainingUpdateInputs:
+        """prover.rs:236-270."""
+        half = trace.width() // 2
+        rows = trace.length()
+        return TrainingUpdateInputs(
+            [trace.get(c, 0) for c in range(half)], [trace.get(c, rows - 1) for c in range(half)],
+            self.trace_length - 1, [list(r) for r in self.x_batch], [list(r) for r in self.y_batch],
+            self.learning_rate, self.precision, self.batch_size)
