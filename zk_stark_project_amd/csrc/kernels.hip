@@ -13,6 +13,7 @@
 #include "zkp_internal.hpp"
 #include "blake3.hpp"
 
+#include <algorithm>
 #include <type_traits>
 
 using namespace fp;
@@ -173,17 +174,64 @@ __device__ __forceinline__ void bfly(felt& x, felt& y, felt w) {
   }
 }
 
-template <bool DIT, int NT>
+#ifdef ZKP_EXP_NOBFLY
+#define ZKP_EXP_NOBFLY_ON true
+#else
+#define ZKP_EXP_NOBFLY_ON false
+#endif
+
+// rounds of a K-stage pass: <= 3 stages each, larger first
+template <int K>
+struct NttRounds {
+  static constexpr int n = (K + 2) / 3;
+  static constexpr int bits(int r) {
+    int rem = K;
+    for (int i = 0; i < r; i++) {
+      int left = n - i;
+      int b = (rem + left - 1) / left;
+      rem -= b > 3 ? 3 : b;
+    }
+    int left = n - r;
+    int b = (rem + left - 1) / left;
+    return b > 3 ? 3 : b;
+  }
+};
+
+// two independent butterflies with their products interleaved (fpd::mul_x2), so
+// each carry consumer sits two instructions after its producer
+template <bool DIT>
+__device__ __forceinline__ void bfly2(felt& x0, felt& y0, felt w0, felt& x1, felt& y1, felt w1) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  if (DIT) {
+    felt t0, t1;
+    fpd::mul_x2(y0, w0, y1, w1, t0, t1);
+    y0 = sub(x0, t0); x0 = add(x0, t0);
+    y1 = sub(x1, t1); x1 = add(x1, t1);
+  } else {
+    felt d0 = sub(x0, y0), d1 = sub(x1, y1);
+    x0 = add(x0, y0); x1 = add(x1, y1);
+    fpd::mul_x2(d0, w0, d1, w1, y0, y1);
+  }
+#else
+  bfly<DIT>(x0, y0, w0);
+  bfly<DIT>(x1, y1, w1);
+#endif
+}
+
+template <bool DIT, int NT, int KC>
 __global__ __launch_bounds__(NT) void k_ntt8(Ntt8Args a) {
   constexpr int E = NT * 8;
   extern __shared__ felt lds[];
-  const uint32_t T = 1u << a.logT, Tl = 1u << a.logTl, K = a.K, lo = a.lo;
-  const uint32_t TP = T + 1;  // padded LDS row (bank spread)
+  constexpr uint32_t K = KC;
+  constexpr uint32_t logT = 11 - KC;  // E = 2^11 elements per block
+  constexpr uint32_t T = 1u << logT;
+  const uint32_t Tl = 1u << a.logTl, lo = a.lo;
+  constexpr uint32_t TP = T + 1;  // padded LDS row (bank spread)
   const uint32_t bidx = blockIdx.y;
   const felt* src = a.src + (uint64_t)(bidx / a.src_div) * a.src_stride;
   felt* dst = a.dst + (uint64_t)bidx * a.dst_stride;
   const felt* scale = a.scale ? a.scale + ((uint64_t)(bidx % a.scale_mod) << a.logn) : nullptr;
-  const uint64_t g0 = (uint64_t)blockIdx.x << a.logT;
+  const uint64_t g0 = (uint64_t)blockIdx.x << logT;
   const uint64_t hi0 = g0 >> lo;
   const uint64_t l0 = (Tl == T) ? (g0 & ((1ull << lo) - 1)) : 0;
   const uint32_t qmask = (1u << K) - 1;
@@ -196,11 +244,38 @@ __global__ __launch_bounds__(NT) void k_ntt8(Ntt8Args a) {
     return ((hi0 + hl) << (lo + K)) + ((uint64_t)q << lo) + l0 + ll;
   };
   (void)qmask;
+  // Passes whose groups have < 8 contiguous felts (lo < 3, e.g. the first DIT
+  // pass) would make every lane of a direct load/store touch its own 128-B
+  // line; those go through LDS in (ll, q, hl) order, contiguous along the wave.
+  const bool staged = a.logTl < 3;
+  auto staged_elem = [&](uint32_t e, uint32_t& slot) -> uint64_t {
+    uint32_t ll = e & (Tl - 1), rest = e >> a.logTl;
+    uint32_t q = rest & ((1u << K) - 1), hl = rest >> K;
+    slot = q * TP + hl * Tl + ll;
+    return ((hi0 + hl) << (lo + K)) + ((uint64_t)q << lo) + l0 + ll;
+  };
+  if (staged) {
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      uint32_t slot;
+      uint64_t ad = staged_elem(tid + i * NT, slot);
+#ifdef ZKP_EXP_NOGMEM
+      felt v = fp::make(ad, (uint64_t)i);
+      if (scale) v = mul(v, v);
+#else
+      felt v = src[ad];
+      if (scale) v = mul(v, scale[ad]);
+#endif
+      lds[slot] = v;
+    }
+    __syncthreads();
+  }
   uint32_t b0 = DIT ? 0 : K;
-  for (uint32_t r = 0; r < a.nrounds; r++) {
-    const uint32_t rb = a.rbits[r];
+  static_for<0, NttRounds<KC>::n>([&](auto rr) {
+    constexpr int r = decltype(rr)::value;
+    constexpr uint32_t rb = NttRounds<KC>::bits(r);
     if (!DIT) b0 -= rb;
-    const bool first = r == 0, last = r + 1 == a.nrounds;
+    constexpr bool first = r == 0, last = r + 1 == NttRounds<KC>::n;
     if (!first) __syncthreads();
     felt x[8];
     uint32_t ggs[2], qlow[2];
@@ -208,7 +283,7 @@ __global__ __launch_bounds__(NT) void k_ntt8(Ntt8Args a) {
     auto coord_gg = [&](int m) { return ((uint32_t)(m >> rb) << LOGNT | tid) & (T - 1); };
     auto coord_q = [&](int m) {
       uint32_t extra = m >> rb, bf = m & ((1u << rb) - 1);
-      uint32_t qo = ((extra << LOGNT) | tid) >> a.logT;
+      uint32_t qo = ((extra << LOGNT) | tid) >> logT;
       uint32_t ql = qo & ((1u << b0) - 1);
       return ((qo >> b0) << (b0 + rb)) | (bf << b0) | ql;
     };
@@ -216,52 +291,61 @@ __global__ __launch_bounds__(NT) void k_ntt8(Ntt8Args a) {
     for (int m = 0; m < 8; m++) {
       uint32_t extra = m >> rb, bf = m & ((1u << rb) - 1);
       uint32_t c = (extra << LOGNT) | tid;
-      if (first) {  // straight from HBM (coalesced along gg), coset scale fused
+      if (first && !staged) {  // straight from HBM (coalesced along gg), coset scale fused
         uint64_t ad = gaddr(coord_gg(m), coord_q(m));
+#ifdef ZKP_EXP_NOGMEM  // timing experiment only (scripts/ntt_experiments.sh): no HBM reads
+        felt v = fp::make(ad, (uint64_t)m);
+        if (scale) v = mul(v, v);
+#else
         felt v = src[ad];
         if (scale) v = mul(v, scale[ad]);
+#endif
         x[m] = v;
       } else {
         x[m] = lds[coord_q(m) * TP + coord_gg(m)];
       }
-      if (bf == 0 && extra < 2) { ggs[extra] = c & (T - 1); qlow[extra] = (c >> a.logT) & ((1u << b0) - 1); }
+      if (bf == 0 && extra < 2) { ggs[extra] = c & (T - 1); qlow[extra] = (c >> logT) & ((1u << b0) - 1); }
     }
-    if (rb == 3) {
+#ifdef ZKP_EXP_NOBFLY  // timing experiment only: data movement without butterflies
+    if constexpr (false) {
+#else
+    if constexpr (rb == 3) {
+#endif
       const uint64_t l = l0 + (ggs[0] & (Tl - 1));
       const uint64_t jb = ((uint64_t)qlow[0] << lo) | l;
       const uint64_t jstep = 1ull << (b0 + lo);
       if (DIT) {
         {
           felt w0 = ntt_tw<true>(a, jb, b0);
-          bfly<true>(x[0], x[1], w0); bfly<true>(x[2], x[3], w0); bfly<true>(x[4], x[5], w0); bfly<true>(x[6], x[7], w0);
+          bfly2<true>(x[0], x[1], w0, x[2], x[3], w0); bfly2<true>(x[4], x[5], w0, x[6], x[7], w0);
         }
         {
           felt w1a = ntt_tw<true>(a, jb, b0 + 1);
-          bfly<true>(x[0], x[2], w1a); bfly<true>(x[4], x[6], w1a);
           felt w1b = ntt_tw<true>(a, jb | jstep, b0 + 1);
-          bfly<true>(x[1], x[3], w1b); bfly<true>(x[5], x[7], w1b);
+          bfly2<true>(x[0], x[2], w1a, x[1], x[3], w1b); bfly2<true>(x[4], x[6], w1a, x[5], x[7], w1b);
         }
-        static_for<0, 4>([&](auto k2) {
-          felt w2 = ntt_tw<true>(a, jb | ((uint64_t)k2 << (b0 + lo)), b0 + 2);
-          bfly<true>(x[k2], x[k2 + 4], w2);
+        static_for<0, 2>([&](auto k2) {
+          felt w2a = ntt_tw<true>(a, jb | ((uint64_t)(2 * k2) << (b0 + lo)), b0 + 2);
+          felt w2b = ntt_tw<true>(a, jb | ((uint64_t)(2 * k2 + 1) << (b0 + lo)), b0 + 2);
+          bfly2<true>(x[2 * k2], x[2 * k2 + 4], w2a, x[2 * k2 + 1], x[2 * k2 + 5], w2b);
         });
       } else {
-        static_for<0, 4>([&](auto k2) {
-          felt w2 = ntt_tw<false>(a, jb | ((uint64_t)k2 << (b0 + lo)), b0 + 2);
-          bfly<false>(x[k2], x[k2 + 4], w2);
+        static_for<0, 2>([&](auto k2) {
+          felt w2a = ntt_tw<false>(a, jb | ((uint64_t)(2 * k2) << (b0 + lo)), b0 + 2);
+          felt w2b = ntt_tw<false>(a, jb | ((uint64_t)(2 * k2 + 1) << (b0 + lo)), b0 + 2);
+          bfly2<false>(x[2 * k2], x[2 * k2 + 4], w2a, x[2 * k2 + 1], x[2 * k2 + 5], w2b);
         });
         {
           felt w1a = ntt_tw<false>(a, jb, b0 + 1);
-          bfly<false>(x[0], x[2], w1a); bfly<false>(x[4], x[6], w1a);
           felt w1b = ntt_tw<false>(a, jb | jstep, b0 + 1);
-          bfly<false>(x[1], x[3], w1b); bfly<false>(x[5], x[7], w1b);
+          bfly2<false>(x[0], x[2], w1a, x[1], x[3], w1b); bfly2<false>(x[4], x[6], w1a, x[5], x[7], w1b);
         }
         {
           felt w0 = ntt_tw<false>(a, jb, b0);
-          bfly<false>(x[0], x[1], w0); bfly<false>(x[2], x[3], w0); bfly<false>(x[4], x[5], w0); bfly<false>(x[6], x[7], w0);
+          bfly2<false>(x[0], x[1], w0, x[2], x[3], w0); bfly2<false>(x[4], x[5], w0, x[6], x[7], w0);
         }
       }
-    } else if (rb == 2) {
+    } else if constexpr (rb == 2 && !ZKP_EXP_NOBFLY_ON) {
 #pragma unroll
       for (int u = 0; u < 2; u++) {
         const uint64_t l = l0 + (ggs[u] & (Tl - 1));
@@ -270,30 +354,47 @@ __global__ __launch_bounds__(NT) void k_ntt8(Ntt8Args a) {
         felt w1a = ntt_tw<DIT>(a, jb, b0 + 1), w1b = ntt_tw<DIT>(a, jb | (1ull << (b0 + lo)), b0 + 1);
         felt* y = x + 4 * u;
         if (DIT) {
-          bfly<true>(y[0], y[1], w0); bfly<true>(y[2], y[3], w0);
-          bfly<true>(y[0], y[2], w1a); bfly<true>(y[1], y[3], w1b);
+          bfly2<true>(y[0], y[1], w0, y[2], y[3], w0);
+          bfly2<true>(y[0], y[2], w1a, y[1], y[3], w1b);
         } else {
-          bfly<false>(y[0], y[2], w1a); bfly<false>(y[1], y[3], w1b);
-          bfly<false>(y[0], y[1], w0); bfly<false>(y[2], y[3], w0);
+          bfly2<false>(y[0], y[2], w1a, y[1], y[3], w1b);
+          bfly2<false>(y[0], y[1], w0, y[2], y[3], w0);
         }
       }
-    } else {
+    } else if constexpr (!ZKP_EXP_NOBFLY_ON) {
 #pragma unroll
       for (int u = 0; u < 4; u++) {
         uint32_t c = ((uint32_t)u << LOGNT) | tid;
         uint32_t gg = c & (T - 1);
-        uint32_t ql = (c >> a.logT) & ((1u << b0) - 1);
+        uint32_t ql = (c >> logT) & ((1u << b0) - 1);
         const uint64_t jb = ((uint64_t)ql << lo) | (l0 + (gg & (Tl - 1)));
         bfly<DIT>(x[2 * u], x[2 * u + 1], ntt_tw<DIT>(a, jb, b0));
       }
     }
-    if (!last) __syncthreads();  // everyone has read this round's slots
+    if (!last || staged) __syncthreads();  // everyone has read this round's slots
 #pragma unroll
     for (int m = 0; m < 8; m++) {
-      if (last) dst[gaddr(coord_gg(m), coord_q(m))] = x[m];  // straight to HBM
+#ifdef ZKP_EXP_NOGMEM
+      if (last && !staged && x[m].lo == 0x0123456789abcdefull) dst[gaddr(coord_gg(m), coord_q(m))] = x[m];
+#else
+      if (last && !staged) dst[gaddr(coord_gg(m), coord_q(m))] = x[m];  // straight to HBM
+#endif
       else lds[coord_q(m) * TP + coord_gg(m)] = x[m];
     }
     if (DIT) b0 += rb;
+  });
+  if (staged) {  // LDS -> HBM in the contiguous order
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      uint32_t slot;
+      uint64_t ad = staged_elem(tid + i * NT, slot);
+#ifdef ZKP_EXP_NOGMEM
+      if (lds[slot].lo == 0x0123456789abcdefull) dst[ad] = lds[slot];
+#else
+      dst[ad] = lds[slot];
+#endif
+    }
   }
   (void)E;
 }
@@ -1064,8 +1165,11 @@ void launch_ntt(Prof& prof, hipStream_t s, const NttBatch& b, uint32_t logn, boo
   static bool attr_set = false;
   if (!attr_set) {
     size_t maxb = (size_t)(1u << LOGE) * (1 + 1.0 / 8) * sizeof(felt) + 16;
-    (void)hipFuncSetAttribute((const void*)k_ntt8<true, 256>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)maxb);
-    (void)hipFuncSetAttribute((const void*)k_ntt8<false, 256>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)maxb);
+    const void* fns[] = {(const void*)k_ntt8<true, 256, 5>, (const void*)k_ntt8<true, 256, 6>,
+                         (const void*)k_ntt8<true, 256, 7>, (const void*)k_ntt8<true, 256, 8>,
+                         (const void*)k_ntt8<false, 256, 5>, (const void*)k_ntt8<false, 256, 6>,
+                         (const void*)k_ntt8<false, 256, 7>, (const void*)k_ntt8<false, 256, 8>};
+    for (const void* f : fns) (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)maxb);
     attr_set = true;
   }
   // pass sizes: prefer multiples of 3 (whole radix-8 rounds), largest pass last
@@ -1116,12 +1220,28 @@ void launch_ntt(Prof& prof, hipStream_t s, const NttBatch& b, uint32_t logn, boo
     uint64_t groups = 1ull << (logn - K);
     dim3 grid((uint32_t)(groups >> a.logT), b.batches);
     size_t shmem = (size_t)(1u << K) * ((1u << a.logT) + 1) * sizeof(felt);
-    if (dit)
-      LAUNCH(prof, "ntt_dit", s, (double)b.batches * (1ull << logn) * 16.0 * (a.scale ? 3 : 2),
-             hipLaunchKernelGGL((k_ntt8<true, 256>), grid, dim3(256), shmem, s, a));
-    else
-      LAUNCH(prof, "ntt_dif", s, (double)b.batches * (1ull << logn) * 16.0 * (a.scale ? 3 : 2),
-             hipLaunchKernelGGL((k_ntt8<false, 256>), grid, dim3(256), shmem, s, a));
+    // compulsory bytes of this launch: every distinct input array once (the
+    // coefficient arrays are shared by src_div coset batches, the scale table
+    // has scale_mod rows) + every output once
+    const double arr = (double)(1ull << logn) * 16.0;
+    const uint32_t src_arrays = first ? (b.batches + a.src_div - 1) / a.src_div : b.batches;
+    const uint32_t scale_rows = a.scale ? (a.scale_mod < b.batches ? a.scale_mod : b.batches) : 0;
+    const double bytes = arr * ((double)src_arrays + scale_rows + b.batches);
+#define ZKP_NTT8(D, KK)                                                                                  \
+  LAUNCH(prof, D ? "ntt_dit" : "ntt_dif", s, bytes,                                                     \
+         hipLaunchKernelGGL((k_ntt8<D, 256, KK>), grid, dim3(256), shmem, s, a))
+    switch (K * 2 + (dit ? 1 : 0)) {
+      case 11: ZKP_NTT8(true, 5); break;
+      case 13: ZKP_NTT8(true, 6); break;
+      case 15: ZKP_NTT8(true, 7); break;
+      case 17: ZKP_NTT8(true, 8); break;
+      case 10: ZKP_NTT8(false, 5); break;
+      case 12: ZKP_NTT8(false, 6); break;
+      case 14: ZKP_NTT8(false, 7); break;
+      case 16: ZKP_NTT8(false, 8); break;
+      default: abort();  // launch_ntt only plans passes of 5..8 stages
+    }
+#undef ZKP_NTT8
     s0 += K;
   }
 }
