@@ -650,6 +650,34 @@ __global__ __launch_bounds__(TPB) void k_comp_dft(const felt* __restrict__ recv,
   }
 }
 
+// Fiat-Shamir step of the FRI commit loop on the device (winter-crypto
+// DefaultRandomCoin<Blake3_256>: reseed = merge(seed, root), counter = 0; draw
+// = first merge_with_int(seed, ++counter) whose low 16 bytes are < p). `root`
+// is the layer's Merkle root; the host replays the same steps afterwards and
+// checks every alpha. coin = [seed words 0..8), alphas[l], roots[l] (8 words).
+__global__ void k_coin_fri_layer(uint32_t* __restrict__ seed, const uint32_t* __restrict__ root,
+                                 felt* __restrict__ alpha_out, uint32_t* __restrict__ root_out) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  uint32_t m[16], s[8];
+  for (int i = 0; i < 8; i++) { m[i] = seed[i]; m[8 + i] = root[i]; root_out[i] = root[i]; }
+  b3::set_iv(s);
+  b3::compress(s, m, 0, 64, b3::CHUNK_START | b3::CHUNK_END | b3::ROOT);
+  felt a = fp::zero();
+  for (uint32_t ctr = 1; ctr <= 1000; ctr++) {
+    for (int i = 0; i < 8; i++) m[i] = s[i];
+    m[8] = ctr;
+    m[9] = 0;
+    for (int i = 10; i < 16; i++) m[i] = 0;
+    uint32_t o[8];
+    b3::set_iv(o);
+    b3::compress(o, m, 0, 40, b3::CHUNK_START | b3::CHUNK_END | b3::ROOT);
+    felt v = fp::make((uint64_t)o[0] | ((uint64_t)o[1] << 32), (uint64_t)o[2] | ((uint64_t)o[3] << 32));
+    if (!fp::ge_p(v)) { a = v; break; }
+  }
+  *alpha_out = a;
+  for (int i = 0; i < 8; i++) seed[i] = s[i];
+}
+
 struct SeedArg {
   uint32_t w[8];
 };
@@ -936,7 +964,8 @@ __global__ __launch_bounds__(TPB) void k_deep(DeepArgs a, const felt* __restrict
 // local row q = jl*m16 + t' is the natural row r = (j0 + jl) + B*t' whose 16
 // values sit at positions t' + k*m16 of the same coset; out is coset-major.
 __global__ __launch_bounds__(TPB) void k_fri_fold16(const felt* __restrict__ E, uint64_t rows, uint32_t logm16,
-                                                    uint32_t j0, uint32_t logB, felt alpha, felt off_inv,
+                                                    uint32_t j0, uint32_t logB, const felt* __restrict__ alpha_p,
+                                                    felt off_inv,
                                                     const felt* __restrict__ itw_lev,
                                                     const felt* __restrict__ eps_inv, felt* __restrict__ out) {
   const uint64_t q = blockIdx.x * (uint64_t)TPB + threadIdx.x;
@@ -978,7 +1007,7 @@ __global__ __launch_bounds__(TPB) void k_fri_fold16(const felt* __restrict__ E, 
     v[blk] = add(x, y);
     v[blk + 1] = sub(x, y);
   }
-  felt beta = mul(alpha, mul(off_inv, itw_lev[r]));
+  felt beta = mul(*alpha_p, mul(off_inv, itw_lev[r]));
   // Horner over k = 15..0 with u_k = v[rev4(k)]
   // u_k = v[rev4(k)], rev4 = {0,8,4,12,2,10,6,14,1,9,5,13,3,11,7,15}
   felt acc = v[15];
@@ -1411,8 +1440,13 @@ void launch_deep(Prof& prof, hipStream_t s, const DeepArgs& a, felt* out) {
          hipLaunchKernelGGL(k_deep, dim3(blocks_for((N + EVAL_CH - 1) / EVAL_CH)), dim3(TPB), 0, s, a, a.binv, out));
 }
 
+void launch_coin_fri_layer(Prof& prof, hipStream_t s, uint32_t* seed, const uint32_t* root, felt* alpha_out,
+                           uint32_t* root_out) {
+  LAUNCH(prof, "coin", s, 0.0, hipLaunchKernelGGL(k_coin_fri_layer, dim3(1), dim3(64), 0, s, seed, root, alpha_out, root_out));
+}
+
 void launch_fri_fold(Prof& prof, hipStream_t s, const felt* E, uint64_t m16, uint32_t Bl, uint32_t j0,
-                     uint32_t logB, uint32_t F, felt alpha, felt off_inv, const felt* itw, uint32_t logD,
+                     uint32_t logB, uint32_t F, const felt* alpha, felt off_inv, const felt* itw, uint32_t logD,
                      const felt* eps_inv, felt* out) {
   (void)F;  // only 16 is compiled (the reference's fri_folding_factor)
   const felt* lev = itw + ((1ull << (logD - 1)) - 1);  // w_D^-r, r < D/2

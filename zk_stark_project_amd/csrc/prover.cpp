@@ -591,7 +591,8 @@ struct TreeShard {
 // mode 0 = LDE rows (cols columns, n rows per coset), mode 1 = FRI rows (16
 // values, 2^logrows rows per coset). Unsharded sources hold all B cosets.
 void commit_rows(zkp_ctx* ctx, zkp_comm* cm, int mode, const felt* src, uint64_t n, uint32_t cols, uint32_t logB,
-                 uint32_t logrows, bool sharded, const std::string& name, TreeShard& tr, uint8_t root[32]) {
+                 uint32_t logrows, bool sharded, const std::string& name, TreeShard& tr, uint8_t root[32],
+                 bool fetch_root = true) {
   Prof& pf = ctx->prof;
   hipStream_t st = ctx->stream;
   const uint64_t L = 1ull << (logB + logrows);
@@ -601,9 +602,11 @@ void commit_rows(zkp_ctx* ctx, zkp_comm* cm, int mode, const felt* src, uint64_t
     tr.nodes = ctx->buf<uint32_t>(name, (size_t)16 * L);
     if (mode == 0) launch_merkle_lde(pf, st, src, cols, logB, n, tr.nodes, L);
     else launch_merkle_fri(pf, st, src, 1ull << logrows, logB, 16, tr.nodes);
-    ctx->download(root, tr.nodes + 8, 32);
     tr.top.assign(2, {});
-    memcpy(tr.top[1].data(), root, 32);
+    if (fetch_root) {  // otherwise the caller reads nodes[1] later
+      ctx->download(root, tr.nodes + 8, 32);
+      memcpy(tr.top[1].data(), root, 32);
+    }
     return;
   }
   const uint32_t R = cm->world, logR = ilog2(R), logBl = logB - logR;
@@ -967,17 +970,36 @@ int prove_impl(zkp_ctx* ctx, zkp_comm* cm, int air_id, const felt* d_trace, uint
       jc = 0;
       sh = false;
     };
+    // Fiat-Shamir of the commit loop on the device: coin[0..8) = seed, then per
+    // layer alpha (4 words) and root (8 words); no host round trip per layer
+    uint32_t* coin_d = ctx->buf<uint32_t>("fri_coin", 8 + 12 * (size_t)(L + 1));
+    felt* alphas_d = reinterpret_cast<felt*>(coin_d + 8);
+    uint32_t* roots_d = coin_d + 8 + 4 * (size_t)L;
+    {
+      uint32_t sw[8];
+      for (int i = 0; i < 8; i++)
+        sw[i] = (uint32_t)coin.seed[4 * i] | ((uint32_t)coin.seed[4 * i + 1] << 8) |
+                ((uint32_t)coin.seed[4 * i + 2] << 16) | ((uint32_t)coin.seed[4 * i + 3] << 24);
+      ctx->upload(coin_d, sw, 32);
+    }
     for (uint32_t l = 0; l < L; l++) {
       const uint64_t m16 = m / F;
       if (sh && (m16 >> logR) < 16) replicate(l);
       Layer& ly = layers[l];
       ly.E = E; ly.m = m; ly.Bc = Bc; ly.jc = jc; ly.sharded = sh;
+      // sharded layers assemble the root on the host (top levels); it is staged back for the coin
       commit_rows(ctx, cm, 1, E, 0, F, logB, ilog2(m16), sh, "ftree_" + std::to_string(l), ly.tree,
-                  T.fri_roots[l]);
-      coin.reseed(T.fri_roots[l]);
-      felt alpha = coin.draw();
+                  T.fri_roots[l], /*fetch_root=*/sh);
+      const uint32_t* root_src = ly.tree.nodes + 8;
+      if (sh) {
+        uint32_t* staged = roots_d + 8 * (size_t)L;  // scratch slot
+        ctx->upload(staged, T.fri_roots[l], 32);
+        root_src = staged;
+      }
+      launch_coin_fri_layer(pf, st, coin_d, root_src, alphas_d + l, roots_d + 8 * (size_t)l);
       felt* nxt = fe + eo;
-      launch_fri_fold(pf, st, E, m16, Bc, jc, logB, F, alpha, inv(off), ctx->itws(logN), ilog2(D), deps, nxt);
+      launch_fri_fold(pf, st, E, m16, Bc, jc, logB, F, alphas_d + l, inv(off), ctx->itws(logN), ilog2(D), deps,
+                      nxt);
       eo += (uint64_t)Bc * m16;
       E = nxt;
       m = m16;
@@ -986,9 +1008,31 @@ int prove_impl(zkp_ctx* ctx, zkp_comm* cm, int air_id, const felt* d_trace, uint
     }
     if (sh) replicate(L);
     layers[L].E = E; layers[L].m = m; layers[L].Bc = B; layers[L].jc = 0; layers[L].sharded = false;
-    // remainder polynomial (FriProver::set_remainder): interpolate the last layer, keep D/B coefficients
+    // one round trip: roots + device alphas + the last layer
+    std::vector<uint8_t> rb((size_t)L * 32);
+    std::vector<felt> dalpha(L);
     std::vector<felt> cm_vals((size_t)B * m);
-    ctx->download(cm_vals.data(), E, cm_vals.size() * 16);
+    {
+      size_t ab = (size_t)L * 16, rbb = (size_t)L * 32, lb = cm_vals.size() * 16;
+      uint8_t* hp = (uint8_t*)ctx->pinned(ab + rbb + lb + 64);
+      if (L) {
+        HIP_CHECK(hipMemcpyAsync(hp, alphas_d, ab + rbb, hipMemcpyDeviceToHost, st));
+      }
+      HIP_CHECK(hipMemcpyAsync(hp + ab + rbb, E, lb, hipMemcpyDeviceToHost, st));
+      ctx->sync();
+      memcpy(dalpha.data(), hp, ab);
+      memcpy(rb.data(), hp + ab, rbb);
+      memcpy(cm_vals.data(), hp + ab + rbb, lb);
+    }
+    // host transcript replay (the proof's commitments and the coin state)
+    for (uint32_t l = 0; l < L; l++) {
+      memcpy(T.fri_roots[l], rb.data() + 32 * (size_t)l, 32);
+      memcpy(layers[l].tree.top[1].data(), T.fri_roots[l], 32);
+      coin.reseed(T.fri_roots[l]);
+      felt alpha = coin.draw();
+      if (!eq(alpha, dalpha[l])) throw ZkpFail{ZKP_ERR_DEVICE, "device FRI transcript diverged from the host"};
+    }
+    // remainder polynomial (FriProver::set_remainder): interpolate the last layer, keep D/B coefficients
     remainder.resize(D);
     for (uint64_t j = 0; j < B; j++)
       for (uint64_t t = 0; t < m; t++) remainder[j + B * t] = cm_vals[j * m + t];

@@ -152,10 +152,13 @@ struct DeepArgs {
 void launch_deep(Prof& prof, hipStream_t s, const DeepArgs& a, felt* out);
 
 // FRI fold-by-F (F = 16) over coset-major evaluations of the cosets [j0, j0+Bl)
-// (16*m16 positions each): natural row r = j + B*t', x_r = off * w_D^r
+// (16*m16 positions each): natural row r = j + B*t', x_r = off * w_D^r; alpha read from device
 void launch_fri_fold(Prof& prof, hipStream_t s, const felt* E, uint64_t m16, uint32_t Bl, uint32_t j0,
-                     uint32_t logB, uint32_t F, felt alpha, felt off_inv, const felt* itw, uint32_t logD,
+                     uint32_t logB, uint32_t F, const felt* alpha, felt off_inv, const felt* itw, uint32_t logD,
                      const felt* eps_inv_dev, felt* out);
+// device-side coin step of the FRI loop: seed = merge(seed, root); *alpha_out = draw(); root copied to root_out
+void launch_coin_fri_layer(Prof& prof, hipStream_t s, uint32_t* seed, const uint32_t* root, felt* alpha_out,
+                           uint32_t* root_out);
 
 // gathers for query openings
 struct GatherSeg {
