@@ -35,26 +35,31 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 # launch name (zkp_kernel_stats_table) -> kernel symbol in the rocprofv3 PMC
 # summaries that scripts/profile_round.sh writes (profiles/r01_pmc_traffic_*.json)
 KERNEL_SYMBOL = {
-    "ntt_dit": "void k_ntt8<true, 256>", "ntt_dif": "void k_ntt8<false, 256>", "deep": "k_deep",
-    "merkle_lde": "void k_merkle_lane<0, 3>", "eval_mimc": "k_eval_mimc", "eval_linear": "k_eval_linear",
+    "ntt_dit": "void k_ntt8<true,", "ntt_dif": "void k_ntt8<false,", "deep": "k_deep",
+    "merkle_lde": "void k_merkle_lane<0,", "eval_mimc": "k_eval_mimc", "eval_linear": "void k_eval_linear<",
 }
 
 
 def pmc_traffic(kernel: str, air: str, mode: str):
     """HBM bytes per launch (FETCH_SIZE x2 + WRITE_SIZE, gfx950-corrected) of `kernel`
-    from the committed PMC summary of the same workload, or None."""
+    from the committed PMC summary of the same workload, or None. A launch name may
+    cover several template instances (the NTT pass kernels are templated on their
+    stage count): their traffic is averaged over all their launches."""
     if mode != "replicas":
         return None, None
     name = {"mimc": "r01_pmc_traffic_mimc_c2.json", "agg": "r01_pmc_traffic_agg_c3.json"}[air]
     path = os.path.join(ROOT, "profiles", name)
-    sym = KERNEL_SYMBOL.get(kernel)
-    if not sym or not os.path.exists(path):
+    prefix = KERNEL_SYMBOL.get(kernel)
+    if not prefix or not os.path.exists(path):
         return None, None
     with open(path) as f:
-        rec = json.load(f).get(sym)
-    if not rec:
+        recs = {k: v for k, v in json.load(f).items() if k == prefix or k.startswith(prefix)}
+    launches = sum(v["launches"] for v in recs.values())
+    if not launches:
         return None, None
-    return rec["traffic_per_launch"], f"profiles/{name} ({sym}, rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes)"
+    traffic = sum(v["traffic_per_launch"] * v["launches"] for v in recs.values()) / launches
+    syms = ", ".join(sorted(recs))
+    return traffic, f"profiles/{name} ({syms}; rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes)"
 
 
 def parse():

@@ -58,8 +58,22 @@ def main(d):
                   "traffic_per_launch": rd + wr, **stats.get(k, {})}
     with open(os.path.join(d, "traffic.json"), "w") as fh:
         json.dump(res, fh, indent=1)
-    print(f"{'kernel':60s} {'launches':>8s} {'avg_ms':>9s} {'MB/launch':>10s} {'GB/s':>8s}")
+    # families: template instances of one launch site (e.g. the NTT pass kernels,
+    # templated on their stage count) pooled over all their launches, which is
+    # how bench.py's per-launch-name HIP-event averages are formed
+    fam = defaultdict(lambda: {"launches": 0, "traffic": 0.0, "total_ms": 0.0, "calls": 0})
     for k, v in res.items():
+        f = k.split(",")[0] + ("...>" if "," in k else "")
+        fam[f]["launches"] += v["launches"]
+        fam[f]["traffic"] += v["traffic_per_launch"] * v["launches"]
+        fam[f]["total_ms"] += v.get("total_ms", 0.0)
+        fam[f]["calls"] += v.get("calls", 0)
+    families = {f: {"launches": v["launches"], "traffic_per_launch": v["traffic"] / max(v["launches"], 1),
+                    "avg_ms": v["total_ms"] / max(v["calls"], 1)} for f, v in fam.items()}
+    with open(os.path.join(d, "traffic_families.json"), "w") as fh:
+        json.dump(families, fh, indent=1)
+    print(f"{'kernel':60s} {'launches':>8s} {'avg_ms':>9s} {'MB/launch':>10s} {'GB/s':>8s}")
+    for k, v in list(res.items()) + [("[family] " + f, v) for f, v in families.items()]:
         ms = v.get("avg_ms", 0.0)
         gbs = v["traffic_per_launch"] / (ms * 1e6) if ms else 0.0
         print(f"{k[:60]:60s} {v['launches']:8d} {ms:9.4f} {v['traffic_per_launch'] / 1e6:10.2f} {gbs:8.1f}")
