@@ -184,6 +184,31 @@ int zkp_merkle_commit_rows(zkp_ctx* ctx, const zkp_felt* cols, uint32_t width, u
  * smallest nonce >= 1 with trailing_zeros(u64_le(BLAKE3(seed || nonce_le)[0..8])) >= bits. */
 int zkp_grind(zkp_ctx* ctx, const uint8_t seed[32], uint32_t bits, uint64_t* nonce);
 
+/* ---- verification (≙ winterfell `verify`) ------------------------------ */
+/* Status codes of zkp_verify; values map onto winter-verifier `VerifierError`. */
+typedef enum zkp_verify_status {
+  ZKP_VERIFY_OK = 0,
+  ZKP_VERIFY_INCONSISTENT_BASE_FIELD = 32,  /* InconsistentBaseField */
+  ZKP_VERIFY_UNACCEPTABLE_OPTIONS = 33,     /* UnacceptableProofOptions */
+  ZKP_VERIFY_DESERIALIZATION = 34,          /* ProofDeserializationError */
+  ZKP_VERIFY_PUB_INPUTS = 35,               /* public inputs rejected by Air::new */
+  ZKP_VERIFY_INCONSISTENT_OOD = 36,         /* InconsistentOodConstraintEvaluations */
+  ZKP_VERIFY_TRACE_QUERY = 37,              /* TraceQueryDoesNotMatchCommitment */
+  ZKP_VERIFY_CONSTRAINT_QUERY = 38,         /* ConstraintQueryDoesNotMatchCommitment */
+  ZKP_VERIFY_POW = 39,                      /* QuerySeedProofOfWorkVerificationFailed */
+  ZKP_VERIFY_FRI = 40,                      /* FriVerificationFailed */
+  ZKP_VERIFY_RANDOM_COIN = 41               /* RandomCoinError */
+} zkp_verify_status;
+
+/* Checks a proof produced by zkp_prove / zkp_prove_sharded against the public
+ * inputs (`pub_inputs.to_elements()`) and the one acceptable option set.
+ * Replaces `verify::<AIR, Blake3_256<Felt>, DefaultRandomCoin<..>, MerkleTree<..>>(
+ * proof, pub_inputs, &AcceptableOptions::OptionSet(vec![options]))` at
+ * src/main.rs:251-257, 430-436, 478-484. Host-only: needs no device and no ctx.
+ * Returns ZKP_VERIFY_OK, a zkp_verify_status or ZKP_ERR_ARGUMENT. */
+int zkp_verify(zkp_air_id air, const uint8_t* proof, uint64_t proof_len, const zkp_felt* pub_elems,
+               uint64_t n_pub, const zkp_proof_options* acceptable);
+
 /* ---- trace construction helper ---------------------------------------- */
 /* Host-side MiMC AIR trace: out[0] = seed mod p,
  * out[i+1] = (out[i] + K[i % 64])^7 with K[j] = (j+1)*10^6

@@ -71,7 +71,25 @@ EXPORTED = [
     "zkp_set_profiling", "zkp_kernel_stats", "zkp_reset_stats", "zkp_kernel_stats_table",
     "zkp_build_mimc_trace", "zkp_prove_sharded", "zkp_comm_local_group", "zkp_comm_rccl_unique_id",
     "zkp_comm_rccl_create", "zkp_comm_destroy", "zkp_comm_rank", "zkp_comm_world", "zkp_prove_sharded_device",
+    "zkp_verify",
 ]
+
+# zkp_verify_status (include/zkp.h) -> winter-verifier `VerifierError` variant
+VERIFY_STATUS = {
+    32: "InconsistentBaseField", 33: "UnacceptableProofOptions", 34: "ProofDeserializationError",
+    35: "InvalidPublicInputs", 36: "InconsistentOodConstraintEvaluations",
+    37: "TraceQueryDoesNotMatchCommitment", 38: "ConstraintQueryDoesNotMatchCommitment",
+    39: "QuerySeedProofOfWorkVerificationFailed", 40: "FriVerificationFailed", 41: "RandomCoinError",
+}
+
+
+class VerifierError(ValueError):
+    """winter-verifier `VerifierError` (the variant name is in .kind)."""
+
+    def __init__(self, code: int):
+        self.code = code
+        self.kind = VERIFY_STATUS.get(code, STATUS.get(code, "unknown"))
+        super().__init__(f"proof rejected: {self.kind} (status {code})")
 
 _lib = None
 _lock = threading.Lock()
@@ -125,6 +143,8 @@ def load():
         L.zkp_comm_destroy.restype = None
         L.zkp_comm_rank.argtypes = [vp]
         L.zkp_comm_world.argtypes = [vp]
+        L.zkp_verify.argtypes = [i32, ctypes.c_char_p, u64, vp, u64, popt]
+        L.zkp_verify.restype = i32
         _lib = L
         return L
 
@@ -137,6 +157,21 @@ def mimc_trace(seed: int, n: int) -> np.ndarray:
     if rc:
         raise ZkpError(rc, "zkp_build_mimc_trace")
     return out
+
+
+def verify_status(air_id: int, proof: bytes, pub, options: ProofOptions) -> int:
+    """zkp_verify (host-only, no device): 0 or a zkp_verify_status code."""
+    L = load()
+    pub_np = np.array([[v & (2**64 - 1), v >> 64] for v in pub], dtype=np.uint64).reshape(-1, 2)
+    return L.zkp_verify(int(air_id), bytes(proof), len(proof), pub_np.ctypes.data if len(pub) else None,
+                        len(pub), ctypes.byref(options.to_c()))
+
+
+def verify(air_id: int, proof: bytes, pub, options: ProofOptions) -> None:
+    """`winterfell::verify` with `AcceptableOptions::OptionSet(vec![options])`; raises VerifierError."""
+    rc = verify_status(air_id, proof, pub, options)
+    if rc:
+        raise VerifierError(rc)
 
 
 class Comm:

@@ -265,3 +265,28 @@ class TrainingUpdateProver(Prover):
             [trace.get(c, 0) for c in range(half)], [trace.get(c, rows - 1) for c in range(half)],
             self.trace_length - 1, [list(r) for r in self.x_batch], [list(r) for r in self.y_batch],
             self.learning_rate, self.precision, self.batch_size)
+
+
+# ------------------------------------------------------------------ verifier
+def verify(air, proof, pub_inputs, acceptable_options) -> None:
+    """`winterfell::verify::<AIR, Blake3_256, DefaultRandomCoin, MerkleTree>(proof, pub_inputs,
+    &AcceptableOptions::OptionSet(..))` as called at /root/reference/src/main.rs:251-257, 430-436, 478-484.
+
+    `air` is an AIR class (MimcAir, GlobalUpdateAir, TrainingUpdateAir) or its id; `proof` a Proof or
+    its bytes; `pub_inputs` an inputs object (to_elements()) or the element list; `acceptable_options`
+    a ProofOptions or a list of them (OptionSet). Raises `_native.VerifierError` on rejection. Runs in
+    libzkp.so on the host (no device needed)."""
+    air_id = air if isinstance(air, int) else air.AIR_ID
+    data = proof.to_bytes() if isinstance(proof, Proof) else bytes(proof)
+    pub = pub_inputs.to_elements() if hasattr(pub_inputs, "to_elements") else list(pub_inputs)
+    opts = acceptable_options if isinstance(acceptable_options, (list, tuple)) else [acceptable_options]
+    last = None
+    for o in opts:
+        try:
+            _native.verify(air_id, data, pub, o)
+            return
+        except _native.VerifierError as e:
+            last = e
+            if e.kind != "UnacceptableProofOptions":
+                raise
+    raise last
