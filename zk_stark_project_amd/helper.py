@@ -208,3 +208,59 @@ def backward_propagation_layer(w, b, x, output_error, learning_rate, pr, w_sign,
             grad, gs = divide(t, pr, ts, 0)
             w[i][j], w_sign[i][j] = subtract(w[i][j], grad, w_sign[i][j], gs)
     return [r[:] for r in w], b[:], [r[:] for r in w_sign], b_sign[:]
+
+
+# ---------------------------------------------------------- CLI-side inputs
+def read_dataset(file_path: str):
+    """helper.rs:55-80 — CSV rows of width 46 (features = columns 18..27, label = 45)
+    or 10 (features = 0..9, label = 9); unparsable cells read as 0.0."""
+    import csv
+    feats, labs = [], []
+    with open(file_path, newline="") as fh:
+        for rec in csv.reader(fh):
+            if not rec:
+                continue
+            row = []
+            for cell in rec:
+                try:
+                    row.append(float(cell.strip()))
+                except ValueError:
+                    row.append(0.0)
+            if len(row) == 46:
+                feats.append(row[18:27])
+                labs.append(row[45])
+            elif len(row) == 10:
+                feats.append(row[:9])
+                labs.append(row[9])
+            else:
+                raise ValueError(f"Unexpected CSV width {len(row)}")
+    return feats, labs
+
+
+class EdgeDevice:
+    """helper.rs:83-106 — one device's data; next_batch samples p distinct rows."""
+
+    def __init__(self, features, labels, rng=None):
+        import random
+        self.features, self.labels = features, labels
+        self._rng = rng or random.Random()
+
+    def next_batch(self, p: int):
+        n = len(self.labels)
+        idx = self._rng.sample(range(n), min(p, n))
+        return [list(self.features[i]) for i in idx], [self.labels[i] for i in idx]
+
+
+def generate_initial_model(fe: int, ac: int, sigma: float, rng=None):
+    """helper.rs:108-131 — N(0, sigma) weights as (w, w_sign, b, b_sign), scale 1e6.
+    The reference draws from `thread_rng`; `rng` (random.Random) makes it reproducible."""
+    import random
+    rng = rng or random.Random()
+    w = [[0] * fe for _ in range(ac)]
+    ws = [[0] * fe for _ in range(ac)]
+    b, bs = [0] * ac, [0] * ac
+    for j in range(ac):
+        for i in range(fe):
+            w[j][i], ws[j][i] = f64_to_signed_felt(rng.gauss(0.0, sigma), 1e6)
+        b[j], bs[j] = f64_to_signed_felt(rng.gauss(0.0, sigma), 1e6)
+    return w, ws, b, bs
