@@ -216,6 +216,20 @@ int zkp_verify(zkp_air_id air, const uint8_t* proof, uint64_t proof_len, const z
  * `TraceTable` construction in the reference — not part of the proving path. */
 int zkp_build_mimc_trace(const uint8_t seed[16], uint64_t n, zkp_felt* out);
 
+/* GlobalUpdateProver::build_trace on the device (src/aggregation/prover.rs:98-160;
+ * SURVEY.md §8(f) row 4): writes the 120 x n column-major trace into HBM at
+ * d_trace_out (ready for zkp_prove_device). raw_global = flattened raw global
+ * model (54 weights then 6 biases), blinding = the 60 masks (prover.rs:68-72),
+ * local_updates = ndev x 60 flattened local models (row-major), k = the
+ * aggregation factor (pub element 120). Rows: 0 = [masked | 0], 1..ndev =
+ * [masked + k^-1 * prefix sum of (local_i - raw) | local_{r-1} - raw],
+ * ndev+1.. = [final | 0]. n must be a power of two >= max(8, ndev + 2).
+ * final_state (nullable, 60 felts) receives row ndev + 1's masked state, the
+ * `new_global` of GlobalUpdateProver::get_pub_inputs (prover.rs:163-190). */
+int zkp_build_global_update_trace(zkp_ctx* ctx, const zkp_felt* raw_global, const zkp_felt* blinding,
+                                  const zkp_felt* local_updates, uint64_t ndev, zkp_felt k, uint64_t n,
+                                  void* d_trace_out, zkp_felt* final_state /* nullable */);
+
 /* ---- profiling ------------------------------------------------------- */
 /* When enabled, every kernel launch is bracketed with HIP events on the
  * stream it runs on; zkp_kernel_stats reports per-kernel launch count and

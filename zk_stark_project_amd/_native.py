@@ -71,7 +71,7 @@ EXPORTED = [
     "zkp_set_profiling", "zkp_kernel_stats", "zkp_reset_stats", "zkp_kernel_stats_table",
     "zkp_build_mimc_trace", "zkp_prove_sharded", "zkp_comm_local_group", "zkp_comm_rccl_unique_id",
     "zkp_comm_rccl_create", "zkp_comm_destroy", "zkp_comm_rank", "zkp_comm_world", "zkp_prove_sharded_device",
-    "zkp_verify",
+    "zkp_verify", "zkp_build_global_update_trace",
 ]
 
 # zkp_verify_status (include/zkp.h) -> winter-verifier `VerifierError` variant
@@ -145,6 +145,7 @@ def load():
         L.zkp_comm_world.argtypes = [vp]
         L.zkp_verify.argtypes = [i32, ctypes.c_char_p, u64, vp, u64, popt]
         L.zkp_verify.restype = i32
+        L.zkp_build_global_update_trace.argtypes = [vp, vp, vp, vp, u64, Felt, u64, vp, vp]
         _lib = L
         return L
 
@@ -328,6 +329,21 @@ class Context:
                     "zkp_copy_to_host")
 
     # -- stage entry points -------------------------------------------------
+    def build_global_update_trace(self, raw, blinding, local, k: int, n: int, d_out: int):
+        """zkp_build_global_update_trace: GlobalUpdate trace into HBM at d_out; returns the final
+        masked state (60 ints)."""
+        def arr(vals):
+            a = np.array([[v & (2**64 - 1), v >> 64] for v in vals], dtype=np.uint64).reshape(-1, 2)
+            return np.ascontiguousarray(a)
+        r, b = arr(raw), arr(blinding)
+        loc = arr([v for row in local for v in row]) if local else np.zeros((1, 2), dtype=np.uint64)
+        final = np.zeros((60, 2), dtype=np.uint64)
+        kf = Felt(k & (2**64 - 1), k >> 64)
+        rc = self.lib.zkp_build_global_update_trace(self.ptr, r.ctypes.data, b.ctypes.data, loc.ctypes.data,
+                                                    len(local), kf, n, d_out, final.ctypes.data)
+        self._check(rc, "zkp_build_global_update_trace")
+        return [int(lo) | (int(hi) << 64) for lo, hi in final]
+
     def trace_lde_commit(self, trace: np.ndarray, blowup: int, want_lde: bool = True):
         trace = np.ascontiguousarray(trace, dtype=np.uint64)
         w, n = trace.shape[0], trace.shape[1]

@@ -1058,6 +1058,90 @@ __global__ void k_gather_digests(const uint32_t* __restrict__ nodes, const uint6
   }
 }
 
+// ------------------------------------------------- aggregation trace builder
+// GlobalUpdateProver::build_trace on the device (src/aggregation/prover.rs:98-160):
+// S column c (c < 60) at row r = masked_c + kinv * sum_{i < min(r, ndev)} (local_i,c - raw_c),
+// U column c at row r = local_{r-1},c - raw_c for 1 <= r <= ndev, else 0; rows past
+// ndev + 1 repeat row ndev + 1 (the prefix stops growing there, so padding is free).
+// Rows are scanned in tiles of GU_TILE: per-tile sums, a per-column scan of the
+// tile sums, then the tile-local scans with their carry-in.
+constexpr uint32_t GU_D_DEV = 60, GU_RPT = 16, GU_TILE = TPB * GU_RPT;
+
+__device__ __forceinline__ felt gu_step(const felt* __restrict__ masked, const felt* __restrict__ raw,
+                                        const felt* __restrict__ local, uint64_t ndev, felt kinv, uint32_t c,
+                                        uint64_t r) {
+  if (r == 0) return masked[c];
+  if (r > ndev) return zero();
+  return mul(sub(local[(r - 1) * GU_D_DEV + c], raw[c]), kinv);
+}
+
+__global__ __launch_bounds__(TPB) void k_gu_tile_sums(const felt* __restrict__ masked, const felt* __restrict__ raw,
+                                                      const felt* __restrict__ local, uint64_t ndev, felt kinv,
+                                                      uint64_t n, felt* __restrict__ tile_sum) {
+  __shared__ felt s[TPB];
+  const uint32_t c = blockIdx.y;
+  const uint64_t r0 = (uint64_t)blockIdx.x * GU_TILE + (uint64_t)threadIdx.x * GU_RPT;
+  felt acc = zero();
+  for (uint32_t i = 0; i < GU_RPT; i++)
+    if (r0 + i < n && r0 + i <= ndev) acc = add(acc, gu_step(masked, raw, local, ndev, kinv, c, r0 + i));
+  s[threadIdx.x] = acc;
+  __syncthreads();
+  for (uint32_t h = TPB / 2; h >= 1; h >>= 1) {
+    if (threadIdx.x < h) s[threadIdx.x] = add(s[threadIdx.x], s[threadIdx.x + h]);
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) tile_sum[(uint64_t)c * gridDim.x + blockIdx.x] = s[0];
+}
+
+// exclusive scan of the tile sums of column blockIdx.x (serial: tiles are few)
+__global__ void k_gu_tile_scan(felt* tile_sum, uint32_t tiles) {
+  if (threadIdx.x != 0) return;
+  felt* t = tile_sum + (uint64_t)blockIdx.x * tiles;
+  felt acc = zero();
+  for (uint32_t i = 0; i < tiles; i++) {
+    felt v = t[i];
+    t[i] = acc;
+    acc = add(acc, v);
+  }
+}
+
+__global__ __launch_bounds__(TPB) void k_gu_tile_write(const felt* __restrict__ masked, const felt* __restrict__ raw,
+                                                       const felt* __restrict__ local, uint64_t ndev, felt kinv,
+                                                       uint64_t n, const felt* __restrict__ tile_carry,
+                                                       felt* __restrict__ out) {
+  __shared__ felt s[TPB];
+  const uint32_t c = blockIdx.y;
+  const uint64_t base = (uint64_t)blockIdx.x * GU_TILE;
+  felt* col = out + (uint64_t)c * n;
+  if (c >= GU_D_DEV) {  // U columns: the scaled-out update of row r (coalesced across the block)
+    const uint32_t j = c - GU_D_DEV;
+    for (uint32_t i = 0; i < GU_RPT; i++) {
+      const uint64_t r = base + (uint64_t)i * TPB + threadIdx.x;
+      if (r >= n) break;
+      col[r] = (r >= 1 && r <= ndev) ? sub(local[(r - 1) * GU_D_DEV + j], raw[j]) : zero();
+    }
+    return;
+  }
+  // S columns: GU_RPT row blocks of TPB consecutive rows (coalesced), each a
+  // block-wide inclusive scan (LDS) on top of the running carry
+  felt carry = tile_carry[(uint64_t)c * gridDim.x + blockIdx.x];
+  for (uint32_t i = 0; i < GU_RPT; i++) {
+    const uint64_t r = base + (uint64_t)i * TPB + threadIdx.x;
+    felt v = (r < n && r <= ndev) ? gu_step(masked, raw, local, ndev, kinv, c, r) : zero();
+    __syncthreads();
+    s[threadIdx.x] = v;
+    __syncthreads();
+    for (uint32_t d = 1; d < TPB; d <<= 1) {
+      felt a = threadIdx.x >= d ? s[threadIdx.x - d] : zero();
+      __syncthreads();
+      if (threadIdx.x >= d) s[threadIdx.x] = add(s[threadIdx.x], a);
+      __syncthreads();
+    }
+    if (r < n) col[r] = add(carry, s[threadIdx.x]);
+    carry = add(carry, s[TPB - 1]);
+  }
+}
+
 inline uint32_t blocks_for(uint64_t n, uint32_t per_block = TPB) {
   uint64_t b = (n + per_block - 1) / per_block;
   return (uint32_t)(b == 0 ? 1 : b);
@@ -1502,4 +1586,17 @@ void launch_gather_digests(Prof& prof, hipStream_t s, const uint32_t* nodes, con
                            uint64_t count) {
   LAUNCH(prof, "gather", s, count * 40.0,
          hipLaunchKernelGGL(k_gather_digests, dim3(blocks_for(count)), dim3(TPB), 0, s, nodes, idx, out, count));
+}
+
+void launch_gu_trace(Prof& prof, hipStream_t s, const felt* masked, const felt* raw, const felt* local,
+                     uint64_t ndev, felt kinv, uint64_t n, felt* tile_buf, felt* out) {
+  const uint32_t tiles = (uint32_t)((n + GU_TILE - 1) / GU_TILE);
+  LAUNCH(prof, "gu_trace_sums", s, (double)ndev * GU_D_DEV * 16.0,
+         hipLaunchKernelGGL(k_gu_tile_sums, dim3(tiles, GU_D_DEV), dim3(TPB), 0, s, masked, raw, local, ndev, kinv,
+                            n, tile_buf));
+  LAUNCH(prof, "gu_trace_scan", s, (double)tiles * GU_D_DEV * 32.0,
+         hipLaunchKernelGGL(k_gu_tile_scan, dim3(GU_D_DEV), dim3(64), 0, s, tile_buf, tiles));
+  LAUNCH(prof, "gu_trace_write", s, (double)n * 2 * GU_D_DEV * 16.0 + (double)ndev * GU_D_DEV * 16.0,
+         hipLaunchKernelGGL(k_gu_tile_write, dim3(tiles, 2 * GU_D_DEV), dim3(TPB), 0, s, masked, raw, local, ndev,
+                            kinv, n, tile_buf, out));
 }

@@ -1220,6 +1220,44 @@ int zkp_grind(zkp_ctx* ctx, const uint8_t seed[32], uint32_t bits, uint64_t* non
   });
 }
 
+int zkp_build_global_update_trace(zkp_ctx* ctx, const zkp_felt* raw_global, const zkp_felt* blinding,
+                                  const zkp_felt* local_updates, uint64_t ndev, zkp_felt k, uint64_t n,
+                                  void* d_trace_out, zkp_felt* final_state) {
+  return guarded(ctx, [&] {
+    HIP_CHECK(hipSetDevice(ctx->device));
+    if (!raw_global || !blinding || !d_trace_out || (ndev && !local_updates)) return (int)ZKP_ERR_ARGUMENT;
+    if (n < 8 || (n & (n - 1)) || n < ndev + 2) return (int)ZKP_ERR_TRACE_SHAPE;
+    const felt kf = make(k.lo, k.hi);
+    if (is_zero(kf) || ge_p(kf)) return (int)ZKP_ERR_PUB_INPUTS;
+    auto canon = [](const zkp_felt* v, uint64_t cnt) {
+      for (uint64_t i = 0; i < cnt; i++)
+        if (ge_p(make(v[i].lo, v[i].hi))) return false;
+      return true;
+    };
+    if (!canon(raw_global, GU_D) || !canon(blinding, GU_D) || !canon(local_updates, ndev * GU_D))
+      return (int)ZKP_ERR_ARGUMENT;
+    // masked global model (prover.rs:68-79): raw + blinding
+    std::vector<felt> hm(2 * GU_D);
+    for (uint32_t c = 0; c < GU_D; c++) {
+      hm[c] = add(make(raw_global[c].lo, raw_global[c].hi), make(blinding[c].lo, blinding[c].hi));
+      hm[GU_D + c] = make(raw_global[c].lo, raw_global[c].hi);
+    }
+    felt* dm = ctx->buf<felt>("gu_masked_raw", 2 * GU_D);
+    ctx->upload(dm, hm.data(), hm.size() * 16);
+    felt* dl = ctx->buf<felt>("gu_local", ndev ? ndev * GU_D : 1);
+    if (ndev) HIP_CHECK(hipMemcpyAsync(dl, local_updates, ndev * GU_D * 16, hipMemcpyHostToDevice, ctx->stream));
+    const uint64_t tiles = (n + 4095) / 4096;
+    felt* tb = ctx->buf<felt>("gu_tiles", tiles * GU_D);
+    launch_gu_trace(ctx->prof, ctx->stream, dm, dm + GU_D, dl, ndev, inv(kf), n, tb, (felt*)d_trace_out);
+    if (final_state)  // row ndev + 1 of the S columns (the state get_pub_inputs reads, prover.rs:168-172)
+      HIP_CHECK(hipMemcpy2DAsync(final_state, 16, (const felt*)d_trace_out + ndev + 1, n * 16, 16, GU_D,
+                                 hipMemcpyDeviceToHost, ctx->stream));
+    ctx->sync();
+    ctx->collect_prof();
+    return 0;
+  });
+}
+
 int zkp_set_profiling(zkp_ctx* ctx, int enabled) {
   return guarded(ctx, [&] {
     ctx->prof.enabled = enabled != 0;

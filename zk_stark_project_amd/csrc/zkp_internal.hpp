@@ -84,6 +84,13 @@ void launch_merkle_tree(Prof& prof, hipStream_t s, uint32_t* nodes, uint64_t L);
 void launch_grind(Prof& prof, hipStream_t s, const uint32_t* seed_words_dev, uint64_t base, uint64_t count,
                   uint32_t bits, unsigned long long* result);
 
+// ---------------------------------------------------------------- trace building
+// GlobalUpdate trace (120 x n, column-major) from masked/raw global models (60 each),
+// ndev x 60 local models and k^-1 (src/aggregation/prover.rs:98-160); tile_buf holds
+// 60 * ceil(n / 4096) felts
+void launch_gu_trace(Prof& prof, hipStream_t s, const felt* masked, const felt* raw, const felt* local,
+                     uint64_t ndev, felt kinv, uint64_t n, felt* tile_buf, felt* out);
+
 // ---------------------------------------------------------------- constraints
 // Points of a coset-major shard: local index q = c*n + t is cx[c] * w_n^t,
 // cx[c] = g * w_N^(j of local coset c), twn = w_n^t for t < n/2 (the

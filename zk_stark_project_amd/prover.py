@@ -176,11 +176,28 @@ class GlobalUpdateProver(Prover):
         out[:, len(rows):] = packed[:, -1:]
         return TraceTable(out)
 
+    def build_trace_device(self, ctx=None):
+        """build_trace() on the GPU (zkp_build_global_update_trace): returns the device
+        pointer of the 120 x n column-major trace in HBM (caller frees it with
+        ctx.free) and keeps the final state for get_pub_inputs()."""
+        ctx = ctx or self.context()
+        raw = _flatten(self.raw_global_w, self.raw_global_b)
+        local = [_flatten(w, b) for w, b in zip(self.local_w, self.local_b)]
+        n = self.trace_length
+        d = ctx.alloc(2 * D_STATE * n * 16)
+        try:
+            self._final_state = ctx.build_global_update_trace(raw, self.blinding, local, self.k, n, d)
+        except Exception:
+            ctx.free(d)
+            raise
+        return d
+
     def get_pub_inputs(self, trace: TraceTable | None = None) -> GlobalUpdateInputs:
-        """prover.rs:163-190."""
-        rows = self.compute_iterative_trace_augmented()
+        """prover.rs:163-190 (the final state comes from the device builder when it ran)."""
         steps = len(self.local_w) + 2
-        final = rows[steps - 1][:D_STATE]
+        final = getattr(self, "_final_state", None)
+        if final is None:
+            final = self.compute_iterative_trace_augmented()[steps - 1][:D_STATE]
         new_w, new_b = _unflatten(final, AC, FE)
         digest = mimc_hash_matrix(new_w, new_b, get_round_constants())
         return GlobalUpdateInputs(self.masked_global_w, self.masked_global_b, new_w, new_b,
