@@ -1228,7 +1228,7 @@ int zkp_build_global_update_trace(zkp_ctx* ctx, const zkp_felt* raw_global, cons
     if (!raw_global || !blinding || !d_trace_out || (ndev && !local_updates)) return (int)ZKP_ERR_ARGUMENT;
     if (n < 8 || (n & (n - 1)) || n < ndev + 2) return (int)ZKP_ERR_TRACE_SHAPE;
     const felt kf = make(k.lo, k.hi);
-    if (is_zero(kf) || ge_p(kf)) return (int)ZKP_ERR_PUB_INPUTS;
+    if (ge_p(kf)) return (int)ZKP_ERR_PUB_INPUTS;  // k = 0 is accepted: winterfell inv(0) = 0
     auto canon = [](const zkp_felt* v, uint64_t cnt) {
       for (uint64_t i = 0; i < cnt; i++)
         if (ge_p(make(v[i].lo, v[i].hi))) return false;
