@@ -177,23 +177,29 @@ ZKP_HD felt pow_u64(felt b, uint64_t e) {
   return r;
 }
 
-// x^(p-2); inv(0) = 0 like winter-math
-ZKP_HD felt inv(felt a) {
-  // p - 2 = 0xffffffffffffffff_ffffd2ffffffffff
-  felt r = one();
-  felt b = a;
-  uint64_t e = 0xffffd2ffffffffffULL;
-  for (int i = 0; i < 64; i++) {
-    if (e & 1) r = mul(r, b);
-    b = sqr(b);
-    e >>= 1;
+ZKP_HD felt sqr_n(felt a, int k) {
+  for (int i = 0; i < k; i++) a = sqr(a);
+  return a;
+}
+
+// x^(p-2); inv(0) = 0 like winter-math.
+// p - 2 = [1 x 80][1101 0010][1 x 40] (binary, high to low): addition chain on
+// a_k = x^(2^k - 1) — 135 squarings + 13 products (square-and-multiply: 252)
+ZKP_HD felt inv(felt x) {
+  felt a2 = mul(sqr(x), x);
+  felt a4 = mul(sqr_n(a2, 2), a2);
+  felt a8 = mul(sqr_n(a4, 4), a4);
+  felt a16 = mul(sqr_n(a8, 8), a8);
+  felt a32 = mul(sqr_n(a16, 16), a16);
+  felt a64 = mul(sqr_n(a32, 32), a32);
+  felt a40 = mul(sqr_n(a32, 8), a8);
+  felt t = mul(sqr_n(a64, 16), a16);  // a80
+  const int bits[8] = {1, 1, 0, 1, 0, 0, 1, 0};
+  for (int i = 0; i < 8; i++) {
+    t = sqr(t);
+    if (bits[i]) t = mul(t, x);
   }
-  // high limb all ones: r *= b^(2^64 - 1) via square-and-multiply
-  for (int i = 0; i < 64; i++) {
-    r = mul(r, b);
-    b = sqr(b);
-  }
-  return r;
+  return mul(sqr_n(t, 40), a40);
 }
 
 ZKP_HD felt from_u128_bytes(const uint8_t* p) {

@@ -294,13 +294,18 @@ struct BatchPlan {
 inline BatchPlan plan_batch(uint64_t L, const std::vector<uint64_t>& idx) {
   BatchPlan bp;
   bp.depth = ilog2(L);
+  std::vector<uint64_t> sorted_idx(idx);
+  std::sort(sorted_idx.begin(), sorted_idx.end());
   std::vector<uint64_t> norm;
-  for (uint64_t i : idx) norm.push_back(i & ~1ull);
-  std::sort(norm.begin(), norm.end());
+  norm.reserve(idx.size());
+  for (uint64_t i : sorted_idx) norm.push_back(i & ~1ull);
   norm.erase(std::unique(norm.begin(), norm.end()), norm.end());
-  auto has = [&](uint64_t v) { return std::find(idx.begin(), idx.end(), v) != idx.end(); };
+  auto has = [&](uint64_t v) { return std::binary_search(sorted_idx.begin(), sorted_idx.end(), v); };
   bp.paths.resize(norm.size());
+  for (auto& p : bp.paths) p.reserve(bp.depth);
   std::vector<uint64_t> next, cur;
+  next.reserve(norm.size());
+  cur.reserve(norm.size());
   for (size_t i = 0; i < norm.size(); i++) {
     uint64_t a = norm[i];
     bool ha = has(a), hb = has(a + 1);
@@ -309,7 +314,7 @@ inline BatchPlan plan_batch(uint64_t L, const std::vector<uint64_t>& idx) {
     next.push_back((a + L) >> 1);
   }
   for (uint32_t d = 1; d < bp.depth; d++) {
-    cur = next;
+    cur.swap(next);
     next.clear();
     for (size_t i = 0; i < cur.size(); i++) {
       uint64_t node = cur[i], sib = node ^ 1;

@@ -807,6 +807,30 @@ __global__ __launch_bounds__(1024) void k_invert_products(felt* prod, uint32_t n
   }
 }
 
+// Phase 3 for domain-only divisors: writes 1/den of every point into a table
+// (cached per domain in the ctx, so constraint evaluation reads one felt per
+// point instead of redoing the batch inversion every proof).
+__global__ __launch_bounds__(TPB) void k_den_table(PointMap m, uint64_t count, felt c0, felt c1, int two,
+                                                   const felt* __restrict__ binv, felt* __restrict__ out) {
+  __shared__ felt s_pre[TPB], s_suf[TPB];
+  felt den[EVAL_CH];
+  static_for<0, EVAL_CH>([&](auto k) {
+    const uint64_t q = EVAL_POINT(k);
+    den[k] = one();
+    if (q < count) {
+      felt x = point_x(m, q);
+      felt d = sub(x, c0);
+      if (two) d = mul(d, sub(x, c1));
+      den[k] = d;
+    }
+  });
+  block_batch_inverse(den, s_pre, s_suf, binv[blockIdx.x]);
+  static_for<0, EVAL_CH>([&](auto k) {
+    const uint64_t q = EVAL_POINT(k);
+    if (q < count) out[q] = den[k];
+  });
+}
+
 // CE point of local index q (CE-coset-major over the shard's CE cosets):
 // CE coset u = u0 + q/n, row t = q % n, CE index s = u + ce*t, LDE coset
 // j = u * B/ce (local jl = j - j0); the frame rows are t and t+1 of that coset.
@@ -827,15 +851,12 @@ __device__ __forceinline__ CePoint ce_point(const EvalCommon& c, uint64_t q) {
 }
 
 __global__ __launch_bounds__(TPB) void k_eval_mimc(EvalCommon c, MimcEvalArgs a, const felt* __restrict__ lde,
-                                                   const felt* __restrict__ binv, felt* __restrict__ comp) {
-  __shared__ felt s_pre[TPB], s_suf[TPB];
+                                                   const felt* __restrict__ dinv, felt* __restrict__ comp) {
   const uint64_t M = (uint64_t)c.cel << c.logn;
   const uint64_t kmask = (64ull << c.logce) - 1;
-  felt tpart[EVAL_CH], bnum[EVAL_CH], den[EVAL_CH];
   static_for<0, EVAL_CH>([&](auto k) {
-    const uint64_t q0 = EVAL_POINT(k);
-    const bool valid = q0 < M;
-    const uint64_t q = valid ? q0 : 0;
+    const uint64_t q = EVAL_POINT(k);
+    if (q >= M) return;
     const CePoint pt = ce_point(c, q);
     felt cur = lde[pt.off];
     felt nxt = lde[pt.off_next];
@@ -845,14 +866,9 @@ __global__ __launch_bounds__(TPB) void k_eval_mimc(EvalCommon c, MimcEvalArgs a,
     felt u2 = sqr(u), u3 = mul(u2, u), u6 = sqr(u3), u7 = mul(u6, u);
     felt tr = mul(a.coef_t, sub(nxt, u7));
     felt e0 = sub(x, one()), e1 = sub(x, c.w_last);
-    tpart[k] = mul(mul(tr, e1), c.zinv[pt.u]);
-    bnum[k] = add(mul(mul(a.b0, sub(cur, a.v0)), e1), mul(mul(a.b1, sub(cur, a.v1)), e0));
-    den[k] = valid ? mul(e0, e1) : one();
-  });
-  block_batch_inverse(den, s_pre, s_suf, binv[blockIdx.x]);
-  static_for<0, EVAL_CH>([&](auto k) {
-    const uint64_t q = EVAL_POINT(k);
-    if (q < M) comp[q] = add(tpart[k], mul(bnum[k], den[k]));
+    felt tpart = mul(mul(tr, e1), c.zinv[pt.u]);
+    felt bnum = add(mul(mul(a.b0, sub(cur, a.v0)), e1), mul(mul(a.b1, sub(cur, a.v1)), e0));
+    comp[q] = add(tpart, mul(bnum, dinv[q]));  // dinv = 1/((x - 1)(x - w^(n-1)))
   });
 }
 
@@ -862,16 +878,13 @@ __global__ __launch_bounds__(TPB) void k_eval_mimc(EvalCommon c, MimcEvalArgs a,
 // over (x - w_b0); TWO adds group 1 = sum_c beta1_c*cur_c - bconst1 over (x - w_b1).
 template <bool TRANS, bool TWO>
 __global__ __launch_bounds__(TPB) void k_eval_linear(EvalCommon c, LinearEvalArgs a, const felt* __restrict__ lde,
-                                                     const felt* __restrict__ binv, felt* __restrict__ comp) {
-  __shared__ felt s_pre[TPB], s_suf[TPB];
+                                                     const felt* __restrict__ dinv, felt* __restrict__ comp) {
   const uint64_t M = (uint64_t)c.cel << c.logn;
   const uint64_t cstride = 1ull << (c.logn + c.logBl);
   const uint32_t W = a.width;
-  felt tpart[EVAL_CH], bnum[EVAL_CH], den[EVAL_CH];
   static_for<0, EVAL_CH>([&](auto k) {
-    const uint64_t q0 = EVAL_POINT(k);
-    const bool valid = q0 < M;
-    const uint64_t q = valid ? q0 : 0;
+    const uint64_t q = EVAL_POINT(k);
+    if (q >= M) return;
     const CePoint pt = ce_point(c, q);
     const felt* pc = lde + pt.off;
     const felt* pn = lde + pt.off_next;
@@ -883,20 +896,15 @@ __global__ __launch_bounds__(TPB) void k_eval_linear(EvalCommon c, LinearEvalArg
       if (TWO) bs1 = add(bs1, mul(a.coefs[3 * W + col], cur));
     }
     felt x = point_x(c.pm, q);
-    tpart[k] = TRANS ? mul(mul(tr, sub(x, c.w_last)), c.zinv[pt.u]) : zero();
+    felt tpart = TRANS ? mul(mul(tr, sub(x, c.w_last)), c.zinv[pt.u]) : zero();
+    felt bnum;
     if (TWO) {
       felt e0 = sub(x, a.w_bstep), e1 = sub(x, a.w_bstep1);
-      bnum[k] = add(mul(sub(bs0, a.bconst), e1), mul(sub(bs1, a.bconst1), e0));
-      den[k] = valid ? mul(e0, e1) : one();
+      bnum = add(mul(sub(bs0, a.bconst), e1), mul(sub(bs1, a.bconst1), e0));
     } else {
-      bnum[k] = sub(bs0, a.bconst);
-      den[k] = valid ? sub(x, a.w_bstep) : one();
+      bnum = sub(bs0, a.bconst);
     }
-  });
-  block_batch_inverse(den, s_pre, s_suf, binv[blockIdx.x]);
-  static_for<0, EVAL_CH>([&](auto k) {
-    const uint64_t q = EVAL_POINT(k);
-    if (q < M) comp[q] = add(tpart[k], mul(bnum[k], den[k]));
+    comp[q] = add(tpart, mul(bnum, dinv[q]));  // dinv: 1/((x - w^b0)(x - w^b1)) or 1/(x - w^b0)
   });
 }
 
@@ -905,30 +913,110 @@ constexpr uint32_t OOD_LOGE = 11;
 __global__ __launch_bounds__(TPB) void k_eval_bitrev(const felt* __restrict__ arrays, uint32_t logn, uint32_t logE,
                                                      const felt* __restrict__ pw0, const felt* __restrict__ pw1,
                                                      felt* __restrict__ partial) {
-  __shared__ felt s0[1u << OOD_LOGE];
-  __shared__ felt s1[1u << OOD_LOGE];
+  __shared__ felt s0[TPB];
+  __shared__ felt s1[TPB];
   const uint32_t E = 1u << logE;
   const felt* src = arrays + ((uint64_t)blockIdx.y << logn) + ((uint64_t)blockIdx.x << logE);
-  for (uint32_t e = threadIdx.x; e < E; e += TPB) {
-    felt v = src[e];
-    s0[e] = v;
-    s1[e] = v;
+  const uint32_t t = threadIdx.x;
+  // levels 0..2 in registers over the thread's 8 consecutive elements (E = 2048 = 8 * TPB),
+  // the remaining levels over the TPB thread results in LDS
+  uint32_t l = 0, m;
+  if (E == 8 * TPB) {
+    felt v[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) v[i] = src[8 * t + i];
+    felt a[4], b[4];
+    {
+      const felt m0 = pw0[logn - 1], m1 = pw1[logn - 1];
+#pragma unroll
+      for (int i = 0; i < 4; i++) { a[i] = add(v[2 * i], mul(m0, v[2 * i + 1])); b[i] = add(v[2 * i], mul(m1, v[2 * i + 1])); }
+    }
+    {
+      const felt m0 = pw0[logn - 2], m1 = pw1[logn - 2];
+      a[0] = add(a[0], mul(m0, a[1])); a[2] = add(a[2], mul(m0, a[3]));
+      b[0] = add(b[0], mul(m1, b[1])); b[2] = add(b[2], mul(m1, b[3]));
+    }
+    {
+      const felt m0 = pw0[logn - 3], m1 = pw1[logn - 3];
+      s0[t] = add(a[0], mul(m0, a[2]));
+      s1[t] = add(b[0], mul(m1, b[2]));
+    }
+    l = 3;
+    m = TPB;
+  } else {  // smaller blocks: per = E / TPB consecutive elements per thread (or one)
+    const uint32_t per = E >= TPB ? E / TPB : 1;
+    felt v0[8], v1[8];
+    for (uint32_t i = 0; i < per; i++) {
+      felt x = (t * per + i < E) ? src[t * per + i] : zero();
+      v0[i] = x;
+      v1[i] = x;
+    }
+    for (uint32_t w = per; w > 1; w >>= 1, l++) {
+      const felt m0 = pw0[logn - 1 - l], m1 = pw1[logn - 1 - l];
+      for (uint32_t i = 0; i < w / 2; i++) {
+        v0[i] = add(v0[2 * i], mul(m0, v0[2 * i + 1]));
+        v1[i] = add(v1[2 * i], mul(m1, v1[2 * i + 1]));
+      }
+    }
+    s0[t] = v0[0];
+    s1[t] = v1[0];
+    m = E >= TPB ? TPB : E;
   }
   __syncthreads();
-  for (uint32_t l = 0; l < logE; l++) {
-    const uint32_t d = 1u << l;
+  for (uint32_t d = 1; d < m; d <<= 1, l++) {
     const felt m0 = pw0[logn - 1 - l], m1 = pw1[logn - 1 - l];
-    for (uint32_t i = threadIdx.x; i < (E >> (l + 1)); i += TPB) {
-      uint32_t p = i << (l + 1);
+    if (t < m / (2 * d)) {
+      uint32_t p = t * 2 * d;
       s0[p] = add(s0[p], mul(m0, s0[p + d]));
       s1[p] = add(s1[p], mul(m1, s1[p + d]));
     }
     __syncthreads();
   }
-  if (threadIdx.x == 0) {
+  if (t == 0) {
     uint64_t o = ((uint64_t)blockIdx.y * gridDim.x + blockIdx.x) * 2;
     partial[o] = s0[0];
     partial[o + 1] = s1[0];
+  }
+}
+
+// second level of the OOD tree: the nb block partials of each (array, point)
+// (bit-reversed order continues: level logE + l uses pw[logn - 1 - logE - l]);
+// one block per array; nb <= 2 * 2048 (pairs are combined while loading).
+__global__ __launch_bounds__(TPB) void k_eval_bitrev_tail(const felt* __restrict__ partial, uint32_t nb,
+                                                          uint32_t logn, uint32_t logE, const felt* __restrict__ pw0,
+                                                          const felt* __restrict__ pw1, felt ninv,
+                                                          felt* __restrict__ out) {
+  __shared__ felt s0[1u << OOD_LOGE];
+  __shared__ felt s1[1u << OOD_LOGE];
+  const felt* src = partial + (uint64_t)blockIdx.x * nb * 2;
+  uint32_t l = logE, m = nb;
+  if (nb > (1u << OOD_LOGE)) {  // fold one level while loading
+    const felt a0 = pw0[logn - 1 - l], a1 = pw1[logn - 1 - l];
+    for (uint32_t i = threadIdx.x; i < nb / 2; i += TPB) {
+      s0[i] = add(src[4 * i], mul(a0, src[4 * i + 2]));
+      s1[i] = add(src[4 * i + 1], mul(a1, src[4 * i + 3]));
+    }
+    l++;
+    m = nb / 2;
+  } else {
+    for (uint32_t i = threadIdx.x; i < nb; i += TPB) {
+      s0[i] = src[2 * i];
+      s1[i] = src[2 * i + 1];
+    }
+  }
+  __syncthreads();
+  for (uint32_t d = 1; d < m; d <<= 1, l++) {
+    const felt a0 = pw0[logn - 1 - l], a1 = pw1[logn - 1 - l];
+    for (uint32_t i = threadIdx.x; i < m / (2 * d); i += TPB) {
+      uint32_t p = i * 2 * d;
+      s0[p] = add(s0[p], mul(a0, s0[p + d]));
+      s1[p] = add(s1[p], mul(a1, s1[p + d]));
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    out[2 * blockIdx.x] = mul(s0[0], ninv);
+    out[2 * blockIdx.x + 1] = mul(s1[0], ninv);
   }
 }
 
@@ -1480,41 +1568,51 @@ static void launch_den_inverse(Prof& prof, hipStream_t s, const PointMap& m, uin
          hipLaunchKernelGGL(k_invert_products, dim3(1), dim3(1024), 0, s, prod, nb));
 }
 
+static void launch_den_table(Prof& prof, hipStream_t s, const PointMap& m, uint64_t count, felt c0, felt c1,
+                             int two, felt* prod, felt* table) {
+  launch_den_inverse(prof, s, m, count, c0, c1, two, prod);
+  LAUNCH(prof, "den_table", s, (double)count * 16.0,
+         hipLaunchKernelGGL(k_den_table, dim3(blocks_for((count + EVAL_CH - 1) / EVAL_CH)), dim3(TPB), 0, s, m, count,
+                            c0, c1, two, prod, table));
+}
+
 void launch_eval_mimc(Prof& prof, hipStream_t s, const EvalCommon& c, const MimcEvalArgs& a, const felt* lde,
                       felt* comp) {
   uint64_t M = (uint64_t)c.cel << c.logn;
-  if (!a.binv_ready) launch_den_inverse(prof, s, c.pm, M, one(), c.w_last, 1, a.binv);
-  LAUNCH(prof, "eval_mimc", s, (double)M * 32.0,
+  if (!a.binv_ready) launch_den_table(prof, s, c.pm, M, one(), c.w_last, 1, a.binv, a.dinv);
+  LAUNCH(prof, "eval_mimc", s, (double)M * 48.0,
          hipLaunchKernelGGL(k_eval_mimc, dim3(blocks_for((M + EVAL_CH - 1) / EVAL_CH)), dim3(TPB), 0, s, c, a, lde,
-                            a.binv, comp));
+                            a.dinv, comp));
 }
 
 void launch_eval_linear(Prof& prof, hipStream_t s, const EvalCommon& c, const LinearEvalArgs& a, const felt* lde,
                         felt* comp) {
   uint64_t M = (uint64_t)c.cel << c.logn;
   const bool two = a.two_groups;
-  if (!a.binv_ready) launch_den_inverse(prof, s, c.pm, M, a.w_bstep, a.w_bstep1, two ? 1 : 0, a.binv);
+  if (!a.binv_ready) launch_den_table(prof, s, c.pm, M, a.w_bstep, a.w_bstep1, two ? 1 : 0, a.binv, a.dinv);
   dim3 g(blocks_for((M + EVAL_CH - 1) / EVAL_CH));
-  const double bytes = (double)M * (a.width * (a.transition ? 32.0 : 16.0) + 16.0);
+  const double bytes = (double)M * (a.width * (a.transition ? 32.0 : 16.0) + 32.0);
   if (a.transition && !two)
     LAUNCH(prof, "eval_linear", s, bytes,
-           hipLaunchKernelGGL((k_eval_linear<true, false>), g, dim3(TPB), 0, s, c, a, lde, a.binv, comp));
+           hipLaunchKernelGGL((k_eval_linear<true, false>), g, dim3(TPB), 0, s, c, a, lde, a.dinv, comp));
   else if (!a.transition && two)
     LAUNCH(prof, "eval_linear", s, bytes,
-           hipLaunchKernelGGL((k_eval_linear<false, true>), g, dim3(TPB), 0, s, c, a, lde, a.binv, comp));
+           hipLaunchKernelGGL((k_eval_linear<false, true>), g, dim3(TPB), 0, s, c, a, lde, a.dinv, comp));
   else
     LAUNCH(prof, "eval_linear", s, bytes,
-           hipLaunchKernelGGL((k_eval_linear<true, true>), g, dim3(TPB), 0, s, c, a, lde, a.binv, comp));
+           hipLaunchKernelGGL((k_eval_linear<true, true>), g, dim3(TPB), 0, s, c, a, lde, a.dinv, comp));
 }
 
 void launch_eval_bitrev(Prof& prof, hipStream_t s, const felt* arrays, uint32_t narrays, uint32_t logn,
-                        const felt* pw0, const felt* pw1, felt* partial, uint32_t* nblocks_out) {
+                        const felt* pw0, const felt* pw1, felt* partial, felt ninv, felt* out) {
   uint32_t logE = logn < OOD_LOGE ? logn : OOD_LOGE;
   uint32_t nb = 1u << (logn - logE);
-  *nblocks_out = nb;
   LAUNCH(prof, "eval_bitrev", s, (double)narrays * (1ull << logn) * 16.0,
          hipLaunchKernelGGL(k_eval_bitrev, dim3(nb, narrays), dim3(TPB), 0, s, arrays, logn, logE, pw0, pw1,
                             partial));
+  LAUNCH(prof, "eval_bitrev_tail", s, (double)narrays * nb * 32.0,
+         hipLaunchKernelGGL(k_eval_bitrev_tail, dim3(narrays), dim3(TPB), 0, s, partial, nb, logn, logE, pw0, pw1,
+                            ninv, out));
 }
 
 void launch_deep(Prof& prof, hipStream_t s, const DeepArgs& a, felt* out) {

@@ -331,29 +331,19 @@ void ood_eval(zkp_ctx* ctx, const felt* arrays, uint32_t narrays, uint32_t logn,
   felt* dpw = ctx->buf<felt>("ood_pw", 2 * (logn + 1));
   ctx->upload(dpw, pw0.data(), logn * 16);
   ctx->upload(dpw + logn, pw1.data(), logn * 16);
-  uint32_t nb = 0;
   uint32_t logE = logn < 11 ? logn : 11;
+  if (logn - logE > 12) throw ZkpFail{ZKP_ERR_TRACE_SHAPE, "OOD evaluation supports n <= 2^23"};
   felt* part = ctx->buf<felt>("ood_part", (size_t)2 * narrays * (1ull << (logn - logE)));
-  launch_eval_bitrev(ctx->prof, ctx->stream, arrays, narrays, logn, dpw, dpw + logn, part, &nb);
-  std::vector<felt> hp((size_t)2 * narrays * nb);
-  ctx->download(hp.data(), part, hp.size() * 16);
-  felt ninv = inv(felt_u64(1ull << logn));
-  v0.assign(narrays, zero());
-  v1.assign(narrays, zero());
+  felt* dv = ctx->buf<felt>("ood_vals", (size_t)2 * narrays);
+  launch_eval_bitrev(ctx->prof, ctx->stream, arrays, narrays, logn, dpw, dpw + logn, part,
+                     inv(felt_u64(1ull << logn)), dv);
+  std::vector<felt> hv((size_t)2 * narrays);
+  ctx->download(hv.data(), dv, hv.size() * 16);
+  v0.resize(narrays);
+  v1.resize(narrays);
   for (uint32_t arr = 0; arr < narrays; arr++) {
-    for (int k = 0; k < 2; k++) {
-      std::vector<felt> cur(nb);
-      for (uint32_t b2 = 0; b2 < nb; b2++) cur[b2] = hp[((size_t)arr * nb + b2) * 2 + k];
-      const std::vector<felt>& pw = k ? pw1 : pw0;
-      uint32_t l = logE;
-      while (cur.size() > 1) {
-        std::vector<felt> nx(cur.size() / 2);
-        for (size_t i = 0; i < nx.size(); i++) nx[i] = add(cur[2 * i], mul(pw[logn - 1 - l], cur[2 * i + 1]));
-        cur.swap(nx);
-        l++;
-      }
-      (k ? v1 : v0)[arr] = mul(cur[0], ninv);
-    }
+    v0[arr] = hv[2 * arr];
+    v1[arr] = hv[2 * arr + 1];
   }
 }
 
@@ -418,6 +408,7 @@ int prove_impl(zkp_ctx* ctx, zkp_comm* cm, int air_id, const felt* d_trace, uint
     ctx->upload(cx, h.data(), h.size() * 16);
   }
   const felt* twn = ctx->tws(logN) + ((1ull << (logn - 1)) - 1);
+  ctx->stage_end("0_setup");
 
   // 2. trace LDE + commitment (DefaultTraceLde::new): interpolation on every
   // rank, coset LDE of this rank's cosets, sharded row commitment
@@ -471,7 +462,8 @@ int prove_impl(zkp_ctx* ctx, zkp_comm* cm, int air_id, const felt* d_trace, uint
       // divisor inverses depend only on the domain and the assertion steps: cache per config
       std::string key = "binv_mimc_" + dom;
       ma.binv_ready = ctx->have_cached(key);
-      ma.binv = ctx->buf<felt>(key, ((uint64_t)cel * n) / 2048 + 1);
+      ma.binv = ctx->buf<felt>("binv_scratch", ((uint64_t)cel * n) / 2048 + 1);
+      ma.dinv = ctx->buf<felt>(key, (uint64_t)cel * n);
       launch_eval_mimc(pf, st, ec, ma, tlde, comp);
     } else if (air.id == ZKP_AIR_GLOBAL_UPDATE) {
       // GlobalUpdate: T = sum_i a^i (k*next_i - k*cur_i - next_{i+60}); B = sum_c b_c (cur_c - v_c)
@@ -499,7 +491,8 @@ int prove_impl(zkp_ctx* ctx, zkp_comm* cm, int air_id, const felt* d_trace, uint
       la.w_bstep1 = zero();
       std::string key = "binv_lin_" + dom + "_" + std::to_string(air.a_step[0]);
       la.binv_ready = ctx->have_cached(key);
-      la.binv = ctx->buf<felt>(key, ((uint64_t)cel * n) / 2048 + 1);
+      la.binv = ctx->buf<felt>("binv_scratch", ((uint64_t)cel * n) / 2048 + 1);
+      la.dinv = ctx->buf<felt>(key, (uint64_t)cel * n);
       launch_eval_linear(pf, st, ec, la, tlde, comp);
     } else {
       // TrainingUpdate: transitions identically zero; boundary groups at rows 0 and n-1 over
@@ -526,7 +519,8 @@ int prove_impl(zkp_ctx* ctx, zkp_comm* cm, int air_id, const felt* d_trace, uint
       la.w_bstep1 = ec.w_last;
       std::string key = "binv_tu_" + dom;
       la.binv_ready = ctx->have_cached(key);
-      la.binv = ctx->buf<felt>(key, ((uint64_t)cel * n) / 2048 + 1);
+      la.binv = ctx->buf<felt>("binv_scratch", ((uint64_t)cel * n) / 2048 + 1);
+      la.dinv = ctx->buf<felt>(key, (uint64_t)cel * n);
       launch_eval_linear(pf, st, ec, la, tlde, comp);
     }
   }
@@ -860,6 +854,7 @@ int prove_impl(zkp_ctx* ctx, zkp_comm* cm, int air_id, const felt* d_trace, uint
   }
   size_t seg_bytes = segs.size() * sizeof(GatherSeg), idx_bytes = all_idx.size() * 8;
   size_t up_bytes = seg_bytes + idx_bytes, down_bytes = out_words * 4;
+  ctx->stage_end("7a_query_plan");
   uint8_t* hp = (uint8_t*)ctx->pinned(std::max(up_bytes, down_bytes * R) + 64);
   memcpy(hp, segs.data(), seg_bytes);
   memcpy(hp + seg_bytes, all_idx.data(), idx_bytes);
@@ -872,6 +867,7 @@ int prove_impl(zkp_ctx* ctx, zkp_comm* cm, int air_id, const felt* d_trace, uint
   if (R > 1) cm->all_gather(st, dout, dall, down_bytes);
   HIP_CHECK(hipMemcpyAsync(hp, dall, down_bytes * R, hipMemcpyDeviceToHost, st));
   ctx->sync();
+  ctx->stage_end("7b_gather");
   std::vector<uint32_t> gathered(out_words);
   {
     const uint32_t* all = reinterpret_cast<const uint32_t*>(hp);

@@ -114,8 +114,9 @@ struct EvalCommon {
 struct MimcEvalArgs {
   felt coef_t, b0, b1, v0, v1;
   const felt* kper;      // 64*ce periodic values on the CE domain
-  felt* binv;            // one felt per 2048 CE points (per-block inverse products)
-  bool binv_ready;       // binv already holds this domain's values (cached in the ctx)
+  felt* binv;            // scratch: one felt per 2048 CE points (per-block inverse products)
+  felt* dinv;            // M felts: 1/((x - 1)(x - w^(n-1))) per CE point (domain-only, cached in the ctx)
+  bool binv_ready;       // dinv already holds this domain's values
 };
 void launch_eval_mimc(Prof& prof, hipStream_t s, const EvalCommon& c, const MimcEvalArgs& a, const felt* lde,
                       felt* comp);
@@ -129,8 +130,9 @@ struct LinearEvalArgs {
   const felt* coefs;
   felt bconst, w_bstep;
   felt bconst1, w_bstep1;
-  felt* binv;            // one felt per 2048 CE points
-  bool binv_ready;
+  felt* binv;            // scratch: one felt per 2048 CE points
+  felt* dinv;            // M felts: the boundary divisor inverses per CE point (cached in the ctx)
+  bool binv_ready;       // dinv already holds this domain's values
 };
 void launch_eval_linear(Prof& prof, hipStream_t s, const EvalCommon& c, const LinearEvalArgs& a, const felt* lde,
                         felt* comp);
@@ -143,7 +145,7 @@ void launch_comp_dft(Prof& prof, hipStream_t s, const felt* recv, const uint32_t
 // OOD evaluation of bit-reversed arrays (arrays contiguous, stride n) at x0 and x1
 // partial[(a * nblocks + b) * 2 + {0,1}] ; pw0/pw1 = x^(2^l) tables (logn entries, device)
 void launch_eval_bitrev(Prof& prof, hipStream_t s, const felt* arrays, uint32_t narrays, uint32_t logn,
-                        const felt* pw0, const felt* pw1, felt* partial, uint32_t* nblocks_out);
+                        const felt* pw0, const felt* pw1, felt* partial, felt ninv, felt* out);
 
 // DEEP composition over the LDE domain (natural order out)
 struct DeepArgs {
