@@ -134,6 +134,27 @@ ZKP_HD felt mul_portable(felt a, felt b) {
   return reduce8(r);
 }
 
+#if !defined(__HIP_DEVICE_COMPILE__)
+// host path: 64-bit limbs with 128-bit products (x86-64 mulq); same reduction
+// identity 2^128 = C (mod p), applied twice, then one conditional subtraction
+inline felt mul_host(felt a, felt b) {
+  typedef unsigned __int128 u128;
+  const u128 p00 = (u128)a.lo * b.lo, p01 = (u128)a.lo * b.hi, p10 = (u128)a.hi * b.lo, p11 = (u128)a.hi * b.hi;
+  const u128 mid = (p00 >> 64) + (uint64_t)p01 + (uint64_t)p10;
+  const uint64_t w0 = (uint64_t)p00, w1 = (uint64_t)mid;
+  const u128 h = (mid >> 64) + (p01 >> 64) + (p10 >> 64) + p11;  // high 128 bits of the product
+  const u128 t0 = (u128)(uint64_t)h * C + w0;
+  const u128 t1 = (u128)(uint64_t)(h >> 64) * C + w1 + (uint64_t)(t0 >> 64);
+  const u128 x = ((u128)(uint64_t)t1 << 64) | (uint64_t)t0;  // L + H*C = x + x2 * 2^128
+  const uint64_t x2 = (uint64_t)(t1 >> 64);                   // < 2^47
+  u128 s = x + (u128)x2 * C;
+  if (s < x) s += C;  // wrapped past 2^128 (then s < 2^94: no second wrap)
+  const u128 P = ((u128)P_HI << 64) | P_LO;
+  if (s >= P) s -= P;
+  return make((uint64_t)s, (uint64_t)(s >> 64));
+}
+#endif
+
 }  // namespace fp
 
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -161,7 +182,7 @@ ZKP_HD felt mul(felt a, felt b) {
 #if defined(__HIP_DEVICE_COMPILE__)
   return fpd::mul(a, b);
 #else
-  return mul_portable(a, b);
+  return mul_host(a, b);
 #endif
 }
 ZKP_HD felt neg(felt a) { return sub(zero(), a); }

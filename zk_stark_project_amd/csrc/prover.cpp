@@ -437,23 +437,30 @@ int prove_impl(zkp_ctx* ctx, zkp_comm* cm, int air_id, const felt* d_trace, uint
     ec.g = g;
     ec.w_last = pow_u64(wn, n - 1);
     ec.pm = PointMap{cx + B + u0, twn, logn};
-    // 1/(x^n - 1) on the CE domain: x^n = g^n * w_ce^s
-    std::vector<felt> zinv(ce);
-    felt gn = pow_u64(g, n), wce = root_of_unity(logce);
-    for (uint32_t s = 0; s < ce; s++) zinv[s] = inv(sub(mul(gn, pow_u64(wce, s)), one()));
-    felt* dz = ctx->buf<felt>("zinv", ce);
-    ctx->upload(dz, zinv.data(), ce * 16);
+    // 1/(x^n - 1) on the CE domain: x^n = g^n * w_ce^s (domain-only: cached per (n, ce))
+    const std::string zkey = "zinv_" + std::to_string(logn) + "_" + std::to_string(logce);
+    felt* dz = ctx->buf<felt>(zkey, ce);
+    if (!ctx->have_cached(zkey)) {
+      std::vector<felt> zinv(ce);
+      felt gn = pow_u64(g, n), wce = root_of_unity(logce);
+      for (uint32_t s = 0; s < ce; s++) zinv[s] = inv(sub(mul(gn, pow_u64(wce, s)), one()));
+      ctx->upload(dz, zinv.data(), ce * 16);
+    }
     ec.zinv = dz;
     const std::string dom = std::to_string(logn) + "_" + std::to_string(logB) + "_" + std::to_string(u0) + "_" +
                             std::to_string(cel);
     if (air.id == ZKP_AIR_MIMC) {
       // periodic column K over the CE domain: interpolate over <w_64>, evaluate at g^(n/64) * <w_{64 ce}>
-      std::vector<felt> kc(64);
-      for (int j = 0; j < 64; j++) kc[j] = felt_u64((uint64_t)(j + 1) * 1000000ull);
-      host_interpolate(kc, one());
-      std::vector<felt> kv = host_evaluate(kc, 64 * ce, pow_u64(g, n / 64));
-      felt* dk = ctx->buf<felt>("kper", kv.size());
-      ctx->upload(dk, kv.data(), kv.size() * 16);
+      // (domain-only: cached per (n, ce))
+      const std::string kkey = "kper_" + std::to_string(logn) + "_" + std::to_string(logce);
+      felt* dk = ctx->buf<felt>(kkey, 64 * (size_t)ce);
+      if (!ctx->have_cached(kkey)) {
+        std::vector<felt> kc(64);
+        for (int j = 0; j < 64; j++) kc[j] = felt_u64((uint64_t)(j + 1) * 1000000ull);
+        host_interpolate(kc, one());
+        std::vector<felt> kv = host_evaluate(kc, 64 * ce, pow_u64(g, n / 64));
+        ctx->upload(dk, kv.data(), kv.size() * 16);
+      }
       MimcEvalArgs ma;
       ma.coef_t = cc[0];
       ma.b0 = cc[1]; ma.v0 = air.a_val[0];
