@@ -11,7 +11,7 @@ if [ "${1:-build}" = build ]; then
     mkdir -p $ROOT/build_exp/$v
     /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -DZKP_EXP_$v -c $CS/kernels.hip -o $ROOT/build_exp/$v/kernels.o
     /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $ROOT/build_exp/$v/libzkp.so $ROOT/build_exp/$v/kernels.o \
-      $CS/build/prover.o $CS/build/comm.o -Wl,--exclude-libs,ALL -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
+      $CS/build/prover.o $CS/build/verifier.o $CS/build/comm.o -Wl,--exclude-libs,ALL -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
   done
 else
   OUT=$ROOT/gpurun_out/ntt_exp
@@ -22,5 +22,5 @@ else
     timeout -k 10 200 python3 $ROOT/bench.py --stats --no-cpu-baseline --no-verify --steps 5 > $OUT/$v.log 2>&1
     timeout -k 10 200 python3 $ROOT/bench.py --air agg --stats --no-cpu-baseline --no-verify --steps 3 > $OUT/${v}_agg.log 2>&1
   done
-  cp $OUT/libzkp.real.so $ROOT/zk_stark_project_amd/libzkp.so
+  cp $OUT/libzkp.real.so $ROOT/zk_stark_project_amd/libzkp.so; rm -f $OUT/libzkp.real.so
 fi

@@ -226,12 +226,21 @@ __global__ __launch_bounds__(NT) void k_ntt8(Ntt8Args a) {
   constexpr uint32_t logT = 11 - KC;  // E = 2^11 elements per block
   constexpr uint32_t T = 1u << logT;
   const uint32_t Tl = 1u << a.logTl, lo = a.lo;
-  constexpr uint32_t TP = T + 1;  // padded LDS row (bank spread)
-  const uint32_t bidx = blockIdx.y;
+  // LDS rows of T felts (T >= 8), XOR-swizzled by the row's low 3 bits: a wave's
+  // 8-lane groups then hit 8 distinct 16-B bank slots both when lanes walk a row
+  // (compute rounds) and when they walk down a column (staged loads, Tl = 1),
+  // with no padding: 2048 felts = 32 KB per block, 5 blocks per CU
+  auto lidx = [](uint32_t q, uint32_t x) -> uint32_t { return q * T + (x ^ (q & 7u)); };
+  // grid: x = batch (fastest in dispatch order), y = position block. The
+  // batches of one position block run back to back, dealt round-robin over the
+  // 8 XCDs: with B = 8 cosets batch b = col*B + j lands on XCD j, so the
+  // columns of a coset share its scale rows and every batch shares the pass's
+  // twiddles in that XCD's L2 instead of refetching them per array.
+  const uint32_t bidx = blockIdx.x;
   const felt* src = a.src + (uint64_t)(bidx / a.src_div) * a.src_stride;
   felt* dst = a.dst + (uint64_t)bidx * a.dst_stride;
   const felt* scale = a.scale ? a.scale + ((uint64_t)(bidx % a.scale_mod) << a.logn) : nullptr;
-  const uint64_t g0 = (uint64_t)blockIdx.x << logT;
+  const uint64_t g0 = (uint64_t)blockIdx.y << logT;
   const uint64_t hi0 = g0 >> lo;
   const uint64_t l0 = (Tl == T) ? (g0 & ((1ull << lo) - 1)) : 0;
   const uint32_t qmask = (1u << K) - 1;
@@ -251,7 +260,7 @@ __global__ __launch_bounds__(NT) void k_ntt8(Ntt8Args a) {
   auto staged_elem = [&](uint32_t e, uint32_t& slot) -> uint64_t {
     uint32_t ll = e & (Tl - 1), rest = e >> a.logTl;
     uint32_t q = rest & ((1u << K) - 1), hl = rest >> K;
-    slot = q * TP + hl * Tl + ll;
+    slot = lidx(q, hl * Tl + ll);
     return ((hi0 + hl) << (lo + K)) + ((uint64_t)q << lo) + l0 + ll;
   };
   if (staged) {
@@ -302,7 +311,7 @@ __global__ __launch_bounds__(NT) void k_ntt8(Ntt8Args a) {
 #endif
         x[m] = v;
       } else {
-        x[m] = lds[coord_q(m) * TP + coord_gg(m)];
+        x[m] = lds[lidx(coord_q(m), coord_gg(m))];
       }
       if (bf == 0 && extra < 2) { ggs[extra] = c & (T - 1); qlow[extra] = (c >> logT) & ((1u << b0) - 1); }
     }
@@ -379,7 +388,7 @@ __global__ __launch_bounds__(NT) void k_ntt8(Ntt8Args a) {
 #else
       if (last && !staged) dst[gaddr(coord_gg(m), coord_q(m))] = x[m];  // straight to HBM
 #endif
-      else lds[coord_q(m) * TP + coord_gg(m)] = x[m];
+      else lds[lidx(coord_q(m), coord_gg(m))] = x[m];
     }
     if (DIT) b0 += rb;
   });
@@ -1365,7 +1374,7 @@ void launch_ntt(Prof& prof, hipStream_t s, const NttBatch& b, uint32_t logn, boo
   uint32_t npass = (logn + KMAX - 1) / KMAX;
   static bool attr_set = false;
   if (!attr_set) {
-    size_t maxb = (size_t)(1u << LOGE) * (1 + 1.0 / 8) * sizeof(felt) + 16;
+    size_t maxb = (size_t)(1u << LOGE) * sizeof(felt);
     const void* fns[] = {(const void*)k_ntt8<true, 256, 5>, (const void*)k_ntt8<true, 256, 6>,
                          (const void*)k_ntt8<true, 256, 7>, (const void*)k_ntt8<true, 256, 8>,
                          (const void*)k_ntt8<false, 256, 5>, (const void*)k_ntt8<false, 256, 6>,
@@ -1419,8 +1428,8 @@ void launch_ntt(Prof& prof, hipStream_t s, const NttBatch& b, uint32_t logn, boo
       rem -= rb;
     }
     uint64_t groups = 1ull << (logn - K);
-    dim3 grid((uint32_t)(groups >> a.logT), b.batches);
-    size_t shmem = (size_t)(1u << K) * ((1u << a.logT) + 1) * sizeof(felt);
+    dim3 grid(b.batches, (uint32_t)(groups >> a.logT));  // batch fastest (see k_ntt8)
+    size_t shmem = (size_t)(1u << K) * (1u << a.logT) * sizeof(felt);
     // compulsory bytes of this launch: every distinct input array once (the
     // coefficient arrays are shared by src_div coset batches, the scale table
     // has scale_mod rows) + every output once
@@ -1488,7 +1497,10 @@ void merkle_upper(Prof& prof, hipStream_t s, uint32_t* nodes, uint64_t L) {
     MerkleArgs a{};
     a.nodes = nodes;
     a.L = L;
-    if (L >= (1ull << 13)) {
+    // lane passes only while they have >= 2^14 lanes (4 levels, 15 serial merges
+    // per lane); below that the 9-level LDS-fused blocks have the shorter
+    // critical path (9 merges) and fill more CUs
+    if (L >= (1ull << 18)) {
       merkle_pass<2>(prof, s, a, 4, "merkle_upper", (double)L * 32.0 * 1.5);
       L >>= 4;
     } else {
