@@ -1537,6 +1537,15 @@ void launch_merkle_fri(Prof& prof, hipStream_t s, const felt* E, uint64_t m16, u
   a.cols = F;
   a.nodes = nodes;
   a.L = R;
+  if (R <= (1ull << 16)) {
+    // small layers: a lane subtree would serialise 19 compressions per lane on a
+    // few waves; hash 2 rows per thread and build 9 levels per block instead
+    uint64_t blocks = (R + 511) / 512;
+    LAUNCH(prof, "merkle_fri", s, (double)R * (F * 16.0 + 64.0),
+           hipLaunchKernelGGL(k_merkle_fused<1>, dim3((uint32_t)blocks), dim3(256), 0, s, a));
+    merkle_upper(prof, s, nodes, R >= 512 ? R / 512 : 1);
+    return;
+  }
   uint32_t H = 0;
   while (H < 2 && (1ull << (H + 1)) <= R) H++;
   merkle_pass<1>(prof, s, a, H, "merkle_fri", (double)R * (F * 16.0 + 64.0));
@@ -1627,9 +1636,13 @@ void launch_eval_bitrev(Prof& prof, hipStream_t s, const felt* arrays, uint32_t 
                             ninv, out));
 }
 
+void launch_deep_denominators(Prof& prof, hipStream_t s, const PointMap& m, uint64_t count, felt z, felt zg,
+                              felt* binv) {
+  launch_den_inverse(prof, s, m, count, z, zg, 1, binv);
+}
+
 void launch_deep(Prof& prof, hipStream_t s, const DeepArgs& a, felt* out) {
   uint64_t N = 1ull << (a.logn + a.logBl);
-  launch_den_inverse(prof, s, a.pm, N, a.z, a.zg, 1, a.binv);
   LAUNCH(prof, "deep", s, (double)N * ((a.w + a.C) * 16.0 + 16.0),
          hipLaunchKernelGGL(k_deep, dim3(blocks_for((N + EVAL_CH - 1) / EVAL_CH)), dim3(TPB), 0, s, a, a.binv, out));
 }

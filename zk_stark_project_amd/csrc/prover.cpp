@@ -52,6 +52,10 @@ struct DevBuf {
 struct zkp_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
+  // side stream: work that only needs domain data runs there while the main
+  // stream waits on a host round trip (ordered back in with events)
+  hipStream_t side = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   Prof prof;
   std::string err;
   std::map<std::string, DevBuf> bufs;
@@ -249,6 +253,9 @@ struct zkp_ctx {
     if (pinned_p) (void)hipHostFree(pinned_p);
     if (ring_p) (void)hipHostFree(ring_p);
     for (auto e : prof.pool) (void)hipEventDestroy(e);
+    if (ev_fork) (void)hipEventDestroy(ev_fork);
+    if (ev_join) (void)hipEventDestroy(ev_join);
+    if (side) (void)hipStreamDestroy(side);
     if (stream) (void)hipStreamDestroy(stream);
   }
 };
@@ -590,6 +597,14 @@ int prove_impl(zkp_ctx* ctx, zkp_comm* cm, int air_id, const felt* d_trace, uint
   felt z = coin.draw();
   T.z.lo = z.lo; T.z.hi = z.hi;
   felt zg = mul(z, root_of_unity(logn));
+  // the DEEP denominators (x - z)(x - zg) only need z: their batch-inversion
+  // phases run on the side stream while the host finishes the OOD transcript
+  felt* deep_binv = ctx->buf<felt>("binv", ((uint64_t)Bl * n) / 2048 + 1);
+  const PointMap deep_pm{cx + j0, twn, logn};
+  HIP_CHECK(hipEventRecord(ctx->ev_fork, st));
+  HIP_CHECK(hipStreamWaitEvent(ctx->side, ctx->ev_fork, 0));
+  launch_deep_denominators(pf, ctx->side, deep_pm, (uint64_t)Bl * n, z, zg, deep_binv);
+  HIP_CHECK(hipEventRecord(ctx->ev_join, ctx->side));
   std::vector<felt> oz, ozg;
   ood_eval(ctx, coef, w + C, logn, z, zg, oz, ozg);
   std::vector<felt> ood_trace(2 * w);
@@ -616,8 +631,9 @@ int prove_impl(zkp_ctx* ctx, zkp_comm* cm, int air_id, const felt* d_trace, uint
     da.j0 = j0; da.logBl = logBl;
     da.tlde = tlde; da.clde = clde; da.gamma = dg2;
     da.z = z; da.zg = zg; da.kz = kz; da.kzg = kzg; da.g = g;
-    da.pm = PointMap{cx + j0, twn, logn};
-    da.binv = ctx->buf<felt>("binv", ((uint64_t)Bl * n) / 2048 + 1);
+    da.pm = deep_pm;
+    da.binv = deep_binv;
+    HIP_CHECK(hipStreamWaitEvent(st, ctx->ev_join, 0));
     launch_deep(pf, st, da, deep);
   }
   ctx->stage_end("4_deep_launch");
@@ -1005,7 +1021,10 @@ int zkp_ctx_create(int device, zkp_ctx** out) {
   zkp_ctx* c = new (std::nothrow) zkp_ctx();
   if (!c) return ZKP_ERR_OOM;
   c->device = device;
-  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess) {
     delete c;
     return ZKP_ERR_DEVICE;
   }

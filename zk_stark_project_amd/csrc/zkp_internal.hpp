@@ -158,6 +158,10 @@ struct DeepArgs {
   PointMap pm;           // x of the shard's LDE points (cx per owned coset)
   felt* binv;            // scratch: one felt per 2048 LDE points
 };
+// phases 1-2 of the DEEP batch inversion (block inverse products of (x - z)(x - zg)
+// into binv); launch_deep then runs phase 3 + the composition
+void launch_deep_denominators(Prof& prof, hipStream_t s, const PointMap& m, uint64_t count, felt z, felt zg,
+                              felt* binv);
 void launch_deep(Prof& prof, hipStream_t s, const DeepArgs& a, felt* out);
 
 // FRI fold-by-F (F = 16) over coset-major evaluations of the cosets [j0, j0+Bl)
