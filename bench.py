@@ -62,6 +62,28 @@ def pmc_traffic(kernel: str, air: str, mode: str):
     return traffic, f"profiles/{name} ({syms}; rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes)"
 
 
+def valu_side(kernel: str, air: str, mode: str):
+    """VALU issue utilisation of `kernel` (SQ_INSTS_VALU * 4 cycles / (duration * 2.4 GHz * 1024 SIMDs))
+    from the committed SQ PMC summary of the same workload: the path is INT-VALU-bound, so this is the
+    roofline that actually binds."""
+    if mode != "replicas":
+        return None
+    name = {"mimc": "r01_pmc_sq_mimc_c2.json", "agg": "r01_pmc_sq_agg_c3.json"}[air]
+    path = os.path.join(ROOT, "profiles", name)
+    prefix = KERNEL_SYMBOL.get(kernel)
+    if not prefix or not os.path.exists(path):
+        return None
+    with open(path) as f:
+        recs = {k: v for k, v in json.load(f).items() if k == prefix or k.startswith(prefix)}
+    launches = sum(v["launches"] for v in recs.values())
+    if not launches:
+        return None
+    us = sum(v["avg_us"] * v["launches"] for v in recs.values())
+    insts = sum(v["valu_insts_per_launch"] * v["launches"] for v in recs.values())
+    return {"issue_util": round(insts * 4 / (us * 1e3 * 2.4 * 1024), 3), "peak": "1 VALU wave-instruction / 4 cycles / SIMD",
+            "source": f"profiles/{name} (rocprofv3 --pmc SQ_INSTS_VALU, {', '.join(sorted(recs))})"}
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -188,6 +210,7 @@ def main():
         "bytes_per_launch": dom_bytes,
         "avg_launch_ms": round(dom_avg_ms, 5),
         "share_of_device_time": round(dom["ms"] / total_ms, 3) if total_ms else None,
+        "valu": valu_side(dom_name, args.air, args.mode),
     }
 
     cpu = None
@@ -195,17 +218,24 @@ def main():
         import oracle_ref
         tb = trace.to_bytes()
         pb = b"".join(v.to_bytes(16, "little") for v in pub)
+        # bounded sample: whole proofs of the same workload until >= 10 s of CPU work (at most 5)
         t1 = time.perf_counter()
-        cproof, _ = oracle_ref.prove(air_id, tb, width, n, pb, opts)
-        dt = time.perf_counter() - t1
+        count, same = 0, True
+        while True:
+            cproof, _ = oracle_ref.prove(air_id, tb, width, n, pb, opts)
+            count += 1
+            same = same and cproof == proof
+            dt = time.perf_counter() - t1
+            if dt >= 10.0 or count >= 5:
+                break
         cpu = {
-            "value": round(1.0 / dt, 5),
+            "value": round(count / dt, 5),
             "unit": "proofs/s",
             "cores": oracle_ref.lib().oracle_num_threads(),
             "kind": "port",
-            "sample": f"one full proof of the same workload ({workload}) by the C oracle restating the "
-                      f"winterfell 0.12 CPU path (OpenMP), {dt * 1e3:.0f} ms; proof bytes identical to GPU: "
-                      f"{cproof == proof}",
+            "sample": f"{count} full proof(s) of the same workload ({workload}) by the C oracle restating the "
+                      f"winterfell 0.12 CPU path (OpenMP), {dt * 1e3:.0f} ms in all; proof bytes identical to "
+                      f"GPU: {same}",
         }
 
     ms = elapsed / args.steps * 1e3

@@ -45,8 +45,14 @@ def main(d):
         bc = c.get("SQ_LDS_BANK_CONFLICT", 0) / nb if nb else float("nan")
         waves = c.get("SQ_WAVES", 0) / n
         rows.append((us * n, k, n, us, valu, util, lds, bc, waves))
+    out = {}
     for _, k, n, us, valu, util, lds, bc, waves in sorted(rows, reverse=True):
         print(f"{k[:44]:44s} {int(n):6d} {us:8.1f} {valu:12.4g} {util:8.3f} {lds:10.4g} {bc:9.4g} {waves:8.0f}")
+        out[k] = {"launches": int(n), "avg_us": us, "valu_insts_per_launch": valu, "valu_issue_util": util,
+                  "lds_insts_per_launch": lds, "lds_bank_conflicts_per_launch": bc, "waves_per_launch": waves}
+    import json
+    with open(os.path.join(d, "sq.json"), "w") as fh:
+        json.dump(out, fh, indent=1)
 
 
 if __name__ == "__main__":

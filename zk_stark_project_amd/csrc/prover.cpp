@@ -95,6 +95,7 @@ struct zkp_ctx {
   void sync() { HIP_CHECK(hipStreamSynchronize(stream)); }
   // true if `key` was already produced by an earlier call (the caller fills it otherwise)
   std::map<std::string, bool> cached;
+  std::map<std::string, std::vector<felt>> host_cache;  // domain-only host values
   bool have_cached(const std::string& key) {
     bool had = cached[key];
     cached[key] = true;
@@ -446,12 +447,19 @@ int prove_impl(zkp_ctx* ctx, zkp_comm* cm, int air_id, const felt* d_trace, uint
     ec.pm = PointMap{cx + B + u0, twn, logn};
     // 1/(x^n - 1) on the CE domain: x^n = g^n * w_ce^s (domain-only: cached per (n, ce))
     const std::string zkey = "zinv_" + std::to_string(logn) + "_" + std::to_string(logce);
-    felt* dz = ctx->buf<felt>(zkey, ce);
-    if (!ctx->have_cached(zkey)) {
-      std::vector<felt> zinv(ce);
+    std::vector<felt>& zinv = ctx->host_cache[zkey];
+    if (zinv.empty()) {
+      zinv.resize(ce);
       felt gn = pow_u64(g, n), wce = root_of_unity(logce);
       for (uint32_t s = 0; s < ce; s++) zinv[s] = inv(sub(mul(gn, pow_u64(wce, s)), one()));
-      ctx->upload(dz, zinv.data(), ce * 16);
+    }
+    felt* dz = ctx->buf<felt>("zinv_coef", ce);
+    {
+      // MiMC folds its transition coefficient into the per-coset divisor constant
+      std::vector<felt> zc(zinv);
+      if (air.id == ZKP_AIR_MIMC)
+        for (auto& v : zc) v = mul(v, cc[0]);
+      ctx->upload(dz, zc.data(), ce * 16);
     }
     ec.zinv = dz;
     const std::string dom = std::to_string(logn) + "_" + std::to_string(logB) + "_" + std::to_string(u0) + "_" +

@@ -108,7 +108,8 @@ struct EvalCommon {
   uint32_t u0, cel, j0, logBl;
   felt g, w_last;        // domain offset (3), w_n^(n-1)
   PointMap pm;           // x of the shard's CE points (cx per owned CE coset)
-  const felt* zinv;      // ce entries: 1/(x^n - 1) on the CE domain (x^n = g^n * w_ce^s)
+  const felt* zinv;      // ce entries: 1/(x^n - 1) on the CE domain (x^n = g^n * w_ce^s);
+                         // for MiMC pre-multiplied by the transition coefficient
 };
 // MiMC: x' - (x + K)^7 ; boundary steps 0 and n-1 on column 0
 struct MimcEvalArgs {
