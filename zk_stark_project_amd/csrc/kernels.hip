@@ -885,33 +885,57 @@ __global__ __launch_bounds__(TPB) void k_eval_mimc(EvalCommon c, MimcEvalArgs a,
 // (GlobalUpdate); without it the transition part is identically zero
 // (TrainingUpdate). Boundary: group 0 = sum_c beta0_c*cur_c - bconst0
 // over (x - w_b0); TWO adds group 1 = sum_c beta1_c*cur_c - bconst1 over (x - w_b1).
+// LIN_CH points per thread, TPB apart (contiguous per wave); column-outer loop
+// so the LIN_CH (and next-row) loads of a column are in flight together
+constexpr int LIN_CH = 4;
+#define LIN_POINT(k) ((uint64_t)blockIdx.x * (TPB * LIN_CH) + (uint64_t)(k) * TPB + threadIdx.x)
+
 template <bool TRANS, bool TWO>
 __global__ __launch_bounds__(TPB) void k_eval_linear(EvalCommon c, LinearEvalArgs a, const felt* __restrict__ lde,
                                                      const felt* __restrict__ dinv, felt* __restrict__ comp) {
   const uint64_t M = (uint64_t)c.cel << c.logn;
   const uint64_t cstride = 1ull << (c.logn + c.logBl);
   const uint32_t W = a.width;
-  static_for<0, EVAL_CH>([&](auto k) {
-    const uint64_t q = EVAL_POINT(k);
+  uint64_t off[LIN_CH], offn[LIN_CH];
+  felt tr[LIN_CH], bs0[LIN_CH], bs1[LIN_CH];
+  static_for<0, LIN_CH>([&](auto k) {
+    const uint64_t q = LIN_POINT(k) < M ? LIN_POINT(k) : 0;
+    const CePoint pt = ce_point(c, q);
+    off[k] = pt.off;
+    offn[k] = pt.off_next;
+    tr[k] = zero();
+    bs0[k] = zero();
+    bs1[k] = zero();
+  });
+  for (uint32_t col = 0; col < W; col++) {
+    const felt* base = lde + col * cstride;
+    felt cur[LIN_CH];
+    static_for<0, LIN_CH>([&](auto k) { cur[k] = base[off[k]]; });
+    if (TRANS) {
+      felt nxt[LIN_CH];
+      static_for<0, LIN_CH>([&](auto k) { nxt[k] = base[offn[k]]; });
+      const felt ca = a.coefs[col], cb = a.coefs[W + col];
+      static_for<0, LIN_CH>([&](auto k) { tr[k] = add(tr[k], add(mul(ca, nxt[k]), mul(cb, cur[k]))); });
+    }
+    const felt b0 = a.coefs[2 * W + col];
+    static_for<0, LIN_CH>([&](auto k) { bs0[k] = add(bs0[k], mul(b0, cur[k])); });
+    if (TWO) {
+      const felt b1 = a.coefs[3 * W + col];
+      static_for<0, LIN_CH>([&](auto k) { bs1[k] = add(bs1[k], mul(b1, cur[k])); });
+    }
+  }
+  static_for<0, LIN_CH>([&](auto k) {
+    const uint64_t q = LIN_POINT(k);
     if (q >= M) return;
     const CePoint pt = ce_point(c, q);
-    const felt* pc = lde + pt.off;
-    const felt* pn = lde + pt.off_next;
-    felt tr = zero(), bs0 = zero(), bs1 = zero();
-    for (uint32_t col = 0; col < W; col++) {
-      felt cur = pc[col * cstride];
-      if (TRANS) tr = add(tr, add(mul(a.coefs[col], pn[col * cstride]), mul(a.coefs[W + col], cur)));
-      bs0 = add(bs0, mul(a.coefs[2 * W + col], cur));
-      if (TWO) bs1 = add(bs1, mul(a.coefs[3 * W + col], cur));
-    }
     felt x = point_x(c.pm, q);
-    felt tpart = TRANS ? mul(mul(tr, sub(x, c.w_last)), c.zinv[pt.u]) : zero();
+    felt tpart = TRANS ? mul(mul(tr[k], sub(x, c.w_last)), c.zinv[pt.u]) : zero();
     felt bnum;
     if (TWO) {
       felt e0 = sub(x, a.w_bstep), e1 = sub(x, a.w_bstep1);
-      bnum = add(mul(sub(bs0, a.bconst), e1), mul(sub(bs1, a.bconst1), e0));
+      bnum = add(mul(sub(bs0[k], a.bconst), e1), mul(sub(bs1[k], a.bconst1), e0));
     } else {
-      bnum = sub(bs0, a.bconst);
+      bnum = sub(bs0[k], a.bconst);
     }
     comp[q] = add(tpart, mul(bnum, dinv[q]));  // dinv: 1/((x - w^b0)(x - w^b1)) or 1/(x - w^b0)
   });
@@ -1035,17 +1059,36 @@ __global__ __launch_bounds__(TPB) void k_deep(DeepArgs a, const felt* __restrict
   __shared__ felt s_pre[TPB], s_suf[TPB];
   const uint64_t N = 1ull << (a.logn + a.logBl);
   const uint64_t cstride = N;
-  felt num[EVAL_CH], den[EVAL_CH];
+  felt A[EVAL_CH], Bh[EVAL_CH];
+  uint64_t off[EVAL_CH];
   static_for<0, EVAL_CH>([&](auto k) {
     const uint64_t q0 = EVAL_POINT(k);
-    const bool valid = q0 < N;
-    const uint64_t off = valid ? q0 : 0;
-    felt A = zero(), Bh = zero();
-    for (uint32_t c = 0; c < a.w; c++) A = add(A, mul(a.gamma[c], a.tlde[c * cstride + off]));
-    for (uint32_t h = 0; h < a.C; h++) Bh = add(Bh, mul(a.gamma[a.w + h], a.clde[h * cstride + off]));
-    felt x = point_x(a.pm, off);
+    off[k] = q0 < N ? q0 : 0;
+    A[k] = zero();
+    Bh[k] = zero();
+  });
+  // column-outer: the EVAL_CH loads of a column are independent and in flight
+  // together (wide AIRs read w + C columns per point; C3/C5 have 121)
+  for (uint32_t c = 0; c < a.w; c++) {
+    const felt gc = a.gamma[c];
+    const felt* col = a.tlde + c * cstride;
+    felt v[EVAL_CH];
+    static_for<0, EVAL_CH>([&](auto k) { v[k] = col[off[k]]; });
+    static_for<0, EVAL_CH>([&](auto k) { A[k] = add(A[k], mul(gc, v[k])); });
+  }
+  for (uint32_t h = 0; h < a.C; h++) {
+    const felt gh = a.gamma[a.w + h];
+    const felt* col = a.clde + h * cstride;
+    felt v[EVAL_CH];
+    static_for<0, EVAL_CH>([&](auto k) { v[k] = col[off[k]]; });
+    static_for<0, EVAL_CH>([&](auto k) { Bh[k] = add(Bh[k], mul(gh, v[k])); });
+  }
+  felt num[EVAL_CH], den[EVAL_CH];
+  static_for<0, EVAL_CH>([&](auto k) {
+    const bool valid = EVAL_POINT(k) < N;
+    felt x = point_x(a.pm, off[k]);
     felt e1 = sub(x, a.z), e2 = sub(x, a.zg);
-    num[k] = add(mul(sub(add(A, Bh), a.kz), e2), mul(sub(A, a.kzg), e1));
+    num[k] = add(mul(sub(add(A[k], Bh[k]), a.kz), e2), mul(sub(A[k], a.kzg), e1));
     den[k] = valid ? mul(e1, e2) : one();
   });
   block_batch_inverse(den, s_pre, s_suf, binv[blockIdx.x]);
@@ -1611,7 +1654,7 @@ void launch_eval_linear(Prof& prof, hipStream_t s, const EvalCommon& c, const Li
   uint64_t M = (uint64_t)c.cel << c.logn;
   const bool two = a.two_groups;
   if (!a.binv_ready) launch_den_table(prof, s, c.pm, M, a.w_bstep, a.w_bstep1, two ? 1 : 0, a.binv, a.dinv);
-  dim3 g(blocks_for((M + EVAL_CH - 1) / EVAL_CH));
+  dim3 g(blocks_for((M + LIN_CH - 1) / LIN_CH));
   const double bytes = (double)M * (a.width * (a.transition ? 32.0 : 16.0) + 32.0);
   if (a.transition && !two)
     LAUNCH(prof, "eval_linear", s, bytes,
