@@ -175,8 +175,19 @@ def main():
             verified = oracle_ref.verify(air_id, proof, b"".join(v.to_bytes(16, "little") for v in pub),
                                          opts) == 0
 
+    # per-kernel table from two untimed proofs with every launch bracketed; it
+    # names the dominant kernel, whose launches alone carry HIP events in the
+    # timed region (so the roofline is measured live at ~no event overhead)
     ctx.reset_stats()
     ctx.set_profiling(True)
+    for _ in range(2):
+        prove_once()
+    ctx.set_profiling(False)
+    full_stats = ctx.stats_table()
+    kernels = {k: v for k, v in full_stats.items() if not k.startswith("host_")}
+    dom_name = max(kernels.items(), key=lambda kv: kv[1]["ms"])[0]
+    ctx.reset_stats()
+    ctx.set_profiling(True, kernel=dom_name)
     elapsed, _, (proof, tr) = timed_replicas(prove_once, args.steps, max(args.warmup - 1, 0), dist=dist,
                                               device_sync=cuda_sync if dist is not None else None,
                                               device=f"cuda:{local_rank}")
@@ -191,9 +202,8 @@ def main():
         return
 
     host_stages = {k: v for k, v in stats.items() if k.startswith("host_")}
-    stats = {k: v for k, v in stats.items() if not k.startswith("host_")}  # device kernels only
-    total_ms = sum(v["ms"] for v in stats.values())
-    dom_name, dom = max(stats.items(), key=lambda kv: kv[1]["ms"])
+    total_ms = sum(v["ms"] for v in kernels.values())
+    dom = stats[dom_name]  # HIP events of the timed region
     dom_avg_ms = dom["ms"] / dom["launches"]
     dom_bytes = dom["bytes"] / dom["launches"]
     achieved = dom_bytes / (dom_avg_ms * 1e-3) / 1e9
@@ -209,7 +219,7 @@ def main():
         "traffic_source": traffic_src,
         "bytes_per_launch": dom_bytes,
         "avg_launch_ms": round(dom_avg_ms, 5),
-        "share_of_device_time": round(dom["ms"] / total_ms, 3) if total_ms else None,
+        "share_of_device_time": round(kernels[dom_name]["ms"] / total_ms, 3) if total_ms else None,
         "valu": valu_side(dom_name, args.air, args.mode),
     }
 
@@ -270,7 +280,7 @@ def main():
     if args.stats:
         for k, v in sorted(host_stages.items()):
             print(f"{k:26s} calls={v['launches']:6d} wall_ms={v['ms']:9.3f}", file=sys.stderr)
-        for k, v in sorted(stats.items(), key=lambda kv: -kv[1]["ms"]):
+        for k, v in sorted(kernels.items(), key=lambda kv: -kv[1]["ms"]):
             print(f"{k:20s} launches={v['launches']:6d} ms={v['ms']:9.3f} "
                   f"GB/s={v['bytes'] / (v['ms'] * 1e-3) / 1e9 if v['ms'] else 0:9.1f}", file=sys.stderr)
     if dist is not None:

@@ -235,6 +235,9 @@ int zkp_build_global_update_trace(zkp_ctx* ctx, const zkp_felt* raw_global, cons
  * stream it runs on; zkp_kernel_stats reports per-kernel launch count and
  * total device milliseconds since the last reset. */
 int zkp_set_profiling(zkp_ctx* ctx, int enabled);
+/* Restrict the bracketing to launches named `kernel_name` (as in the stats
+ * table, e.g. "ntt_dit"); NULL = every launch. Fewer events in a timed region. */
+int zkp_set_profiling_kernel(zkp_ctx* ctx, const char* kernel_name /* nullable */);
 int zkp_kernel_stats(zkp_ctx* ctx, const char* kernel_name, uint64_t* launches, double* total_ms);
 int zkp_reset_stats(zkp_ctx* ctx);
 /* Returns a newline-separated "name launches total_ms algorithmic_bytes" table (free with zkp_free). */

@@ -71,7 +71,7 @@ EXPORTED = [
     "zkp_set_profiling", "zkp_kernel_stats", "zkp_reset_stats", "zkp_kernel_stats_table",
     "zkp_build_mimc_trace", "zkp_prove_sharded", "zkp_comm_local_group", "zkp_comm_rccl_unique_id",
     "zkp_comm_rccl_create", "zkp_comm_destroy", "zkp_comm_rank", "zkp_comm_world", "zkp_prove_sharded_device",
-    "zkp_verify", "zkp_build_global_update_trace",
+    "zkp_verify", "zkp_build_global_update_trace", "zkp_set_profiling_kernel",
 ]
 
 # zkp_verify_status (include/zkp.h) -> winter-verifier `VerifierError` variant
@@ -128,6 +128,7 @@ def load():
         L.zkp_merkle_commit_rows.argtypes = [vp, vp, u32, u64, ctypes.c_char_p]
         L.zkp_grind.argtypes = [vp, ctypes.c_char_p, u32, ctypes.POINTER(u64)]
         L.zkp_set_profiling.argtypes = [vp, i32]
+        L.zkp_set_profiling_kernel.argtypes = [vp, ctypes.c_char_p]
         L.zkp_kernel_stats.argtypes = [vp, ctypes.c_char_p, ctypes.POINTER(u64), ctypes.POINTER(ctypes.c_double)]
         L.zkp_reset_stats.argtypes = [vp]
         L.zkp_kernel_stats_table.argtypes = [vp, ctypes.POINTER(ctypes.c_char_p)]
@@ -367,7 +368,10 @@ class Context:
         return nonce.value
 
     # -- profiling ----------------------------------------------------------
-    def set_profiling(self, on: bool):
+    def set_profiling(self, on: bool, kernel: str | None = None):
+        """Bracket launches with HIP events (all of them, or only those named `kernel`)."""
+        self._check(self.lib.zkp_set_profiling_kernel(self.ptr, kernel.encode() if kernel else None),
+                    "zkp_set_profiling_kernel")
         self._check(self.lib.zkp_set_profiling(self.ptr, 1 if on else 0), "zkp_set_profiling")
 
     def reset_stats(self):

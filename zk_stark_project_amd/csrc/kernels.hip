@@ -10,6 +10,7 @@
 //    cosets [j0, j0 + Bl) and stores them the same way with B -> Bl, j -> j - j0;
 //  * DEEP / FRI layer evaluations: coset-major too (coset j, position t);
 //  * Merkle trees: nodes[1..2L) of 8-word digests, leaves at nodes[L..2L).
+#include "../../include/zkp.h"
 #include "zkp_internal.hpp"
 #include "blake3.hpp"
 
@@ -664,6 +665,146 @@ __global__ __launch_bounds__(TPB) void k_comp_dft(const felt* __restrict__ recv,
 // = first merge_with_int(seed, ++counter) whose low 16 bytes are < p). `root`
 // is the layer's Merkle root; the host replays the same steps afterwards and
 // checks every alpha. coin = [seed words 0..8), alphas[l], roots[l] (8 words).
+// ---------------------------------------------------------- device transcript
+// winter-crypto DefaultRandomCoin<Blake3_256> on the device: seed = 8 LE words;
+// reseed(d) = BLAKE3(seed || d); draw = first 16 B of BLAKE3(seed || ctr_le64),
+// ctr = 1, 2, ... since the last reseed, rejected while >= p.
+__device__ __forceinline__ void dcoin_reseed(uint32_t s[8], const uint32_t d[8]) {
+  uint32_t m[16];
+  for (int i = 0; i < 8; i++) { m[i] = s[i]; m[8 + i] = d[i]; }
+  b3::set_iv(s);
+  b3::compress(s, m, 0, 64, b3::CHUNK_START | b3::CHUNK_END | b3::ROOT);
+}
+__device__ __forceinline__ felt dcoin_candidate(const uint32_t s[8], uint64_t ctr) {
+  uint32_t m[16], o[8];
+  for (int i = 0; i < 8; i++) m[i] = s[i];
+  m[8] = (uint32_t)ctr;
+  m[9] = (uint32_t)(ctr >> 32);
+  for (int i = 10; i < 16; i++) m[i] = 0;
+  b3::set_iv(o);
+  b3::compress(o, m, 0, 40, b3::CHUNK_START | b3::CHUNK_END | b3::ROOT);
+  return fp::make((uint64_t)o[0] | ((uint64_t)o[1] << 32), (uint64_t)o[2] | ((uint64_t)o[3] << 32));
+}
+// sequential draw (thread-local), advancing *ctr
+__device__ __forceinline__ felt dcoin_draw(const uint32_t s[8], uint64_t* ctr) {
+  for (int i = 0; i < 1000; i++) {
+    felt v = dcoin_candidate(s, ++*ctr);
+    if (!fp::ge_p(v)) return v;
+  }
+  return fp::zero();
+}
+
+// reseed with the trace root, then the constraint composition coefficients
+// (ConstraintCompositionCoefficients::draw: Linear = n draws, Algebraic = powers
+// of one draw, Horner = the powers reversed). One block; Linear draws run in
+// parallel with a sequential redo if any candidate was rejected.
+__global__ __launch_bounds__(TPB) void k_dt_draw_coeffs(uint32_t* __restrict__ seed, const uint32_t* __restrict__ root,
+                                                        uint32_t method, uint32_t ncoef, felt* __restrict__ cc) {
+  __shared__ uint32_t s[8];
+  __shared__ felt alpha;
+  __shared__ int rejected;
+  if (threadIdx.x == 0) {
+    uint32_t t[8], d[8];
+    for (int i = 0; i < 8; i++) { t[i] = seed[i]; d[i] = root[i]; }
+    dcoin_reseed(t, d);
+    for (int i = 0; i < 8; i++) { s[i] = t[i]; seed[i] = t[i]; }
+    rejected = 0;
+    if (method != ZKP_BATCHING_LINEAR) {
+      uint64_t ctr = 0;
+      alpha = dcoin_draw(t, &ctr);
+    }
+  }
+  __syncthreads();
+  uint32_t t[8];
+  for (int i = 0; i < 8; i++) t[i] = s[i];
+  if (method == ZKP_BATCHING_LINEAR) {
+    for (uint32_t i = threadIdx.x; i < ncoef; i += TPB) {
+      felt v = dcoin_candidate(t, (uint64_t)i + 1);
+      if (fp::ge_p(v)) rejected = 1;
+      cc[i] = v;
+    }
+    __syncthreads();
+    if (rejected && threadIdx.x == 0) {  // probability ~2^-82 per draw: redo sequentially
+      uint64_t ctr = 0;
+      for (uint32_t i = 0; i < ncoef; i++) cc[i] = dcoin_draw(t, &ctr);
+    }
+    return;
+  }
+  const felt a = alpha;
+  for (uint32_t i = threadIdx.x; i < ncoef; i += TPB)
+    cc[method == ZKP_BATCHING_HORNER ? ncoef - 1 - i : i] = fp::pow_u64(a, i);
+}
+
+// coefficient-dependent constants of the constraint evaluation kernels, from cc:
+//  MIMC  : out[u] = zinv[u] * cc[0] (u < ce), out[ce] = cc[1], out[ce+1] = cc[2]
+//  GLOBAL_UPDATE (w = 120): out[0..4w) = lin coefs, out[4w] = sum_c cc[num_t+c]*aval[c], out[4w+1] = 0
+//  TRAINING_UPDATE (half = w/2): out[0..4half) = lin coefs, out[4half] / [4half+1] = the two boundary sums
+__global__ __launch_bounds__(TPB) void k_dt_eval_consts(int air, const felt* __restrict__ cc, felt k,
+                                                        const felt* __restrict__ aval, const felt* __restrict__ zinv,
+                                                        uint32_t ce, uint32_t w, uint32_t num_t,
+                                                        felt* __restrict__ out) {
+  __shared__ felt red0[TPB], red1[TPB];
+  const uint32_t t = threadIdx.x;
+  if (air == ZKP_AIR_MIMC) {
+    for (uint32_t u = t; u < ce; u += TPB) out[u] = mul(zinv[u], cc[0]);
+    if (t == 0) { out[ce] = cc[1]; out[ce + 1] = cc[2]; }
+    return;
+  }
+  const bool gu = air == ZKP_AIR_GLOBAL_UPDATE;
+  const uint32_t W = gu ? w : w / 2;  // columns the kernel reads
+  felt s0 = zero(), s1 = zero();
+  for (uint32_t c = t; c < W; c += TPB) {
+    felt a = zero(), b = zero(), b0 = zero(), b1 = zero();
+    if (gu) {
+      const uint32_t d = W / 2;  // 60 state columns, then 60 update columns
+      if (c < d) { a = mul(cc[c], k); b = neg(a); }
+      else a = neg(cc[c - d]);
+      b0 = cc[num_t + c];
+      s0 = add(s0, mul(b0, aval[c]));
+    } else {
+      b0 = cc[num_t + c];
+      b1 = cc[num_t + W + c];
+      s0 = add(s0, mul(b0, aval[c]));
+      s1 = add(s1, mul(b1, aval[W + c]));
+    }
+    out[c] = a;
+    out[W + c] = b;
+    out[2 * W + c] = b0;
+    out[3 * W + c] = b1;
+  }
+  red0[t] = s0;
+  red1[t] = s1;
+  __syncthreads();
+  for (uint32_t h = TPB / 2; h >= 1; h >>= 1) {
+    if (t < h) { red0[t] = add(red0[t], red0[t + h]); red1[t] = add(red1[t], red1[t + h]); }
+    __syncthreads();
+  }
+  if (t == 0) { out[4 * W] = red0[0]; out[4 * W + 1] = red1[0]; }
+}
+
+// reseed with the constraint root, draw z; zz = (z, z*w_n); pw tables
+// pw[l] = z^(2^l), pw[logn + l] = (z w_n)^(2^l) for the OOD evaluation
+__global__ void k_dt_draw_z(uint32_t* __restrict__ seed, const uint32_t* __restrict__ root, felt wn, uint32_t logn,
+                            felt* __restrict__ zz, felt* __restrict__ pw) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  uint32_t t[8], d[8];
+  for (int i = 0; i < 8; i++) { t[i] = seed[i]; d[i] = root[i]; }
+  dcoin_reseed(t, d);
+  for (int i = 0; i < 8; i++) seed[i] = t[i];
+  uint64_t ctr = 0;
+  felt z = dcoin_draw(t, &ctr);
+  felt zg = mul(z, wn);
+  zz[0] = z;
+  zz[1] = zg;
+  felt a = z, b = zg;
+  for (uint32_t l = 0; l < logn; l++) {
+    pw[l] = a;
+    pw[logn + l] = b;
+    a = sqr(a);
+    b = sqr(b);
+  }
+}
+
 __global__ void k_coin_fri_layer(uint32_t* __restrict__ seed, const uint32_t* __restrict__ root,
                                  felt* __restrict__ alpha_out, uint32_t* __restrict__ root_out) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
@@ -756,8 +897,12 @@ __device__ __forceinline__ void block_batch_inverse(felt* v, felt* s_pre, felt* 
 // local points q (EVAL_POINT), x_q = point_x(m, q). Same point->block mapping
 // as the phase-3 kernels.
 __global__ __launch_bounds__(TPB) void k_den_products(PointMap m, uint64_t count, felt c0, felt c1, int two,
-                                                      felt* __restrict__ prod) {
+                                                      const felt* __restrict__ cdev, felt* __restrict__ prod) {
   __shared__ felt s[TPB];
+  if (cdev) {  // points drawn on the device (DEEP: z, z*w_n)
+    c0 = cdev[0];
+    c1 = cdev[1];
+  }
   felt acc = one();
   static_for<0, EVAL_CH>([&](auto k) {
     const uint64_t q = EVAL_POINT(k);
@@ -863,6 +1008,7 @@ __global__ __launch_bounds__(TPB) void k_eval_mimc(EvalCommon c, MimcEvalArgs a,
                                                    const felt* __restrict__ dinv, felt* __restrict__ comp) {
   const uint64_t M = (uint64_t)c.cel << c.logn;
   const uint64_t kmask = (64ull << c.logce) - 1;
+  const felt b0 = a.bcoef[0], b1 = a.bcoef[1];
   static_for<0, EVAL_CH>([&](auto k) {
     const uint64_t q = EVAL_POINT(k);
     if (q >= M) return;
@@ -876,7 +1022,7 @@ __global__ __launch_bounds__(TPB) void k_eval_mimc(EvalCommon c, MimcEvalArgs a,
     felt tr = sub(nxt, u7);  // coef_t is folded into c.zinv (per CE coset)
     felt e0 = sub(x, one()), e1 = sub(x, c.w_last);
     felt tpart = mul(mul(tr, e1), c.zinv[pt.u]);
-    felt bnum = add(mul(mul(a.b0, sub(cur, a.v0)), e1), mul(mul(a.b1, sub(cur, a.v1)), e0));
+    felt bnum = add(mul(mul(b0, sub(cur, a.v0)), e1), mul(mul(b1, sub(cur, a.v1)), e0));
     comp[q] = add(tpart, mul(bnum, dinv[q]));  // dinv = 1/((x - 1)(x - w^(n-1)))
   });
 }
@@ -924,6 +1070,7 @@ __global__ __launch_bounds__(TPB) void k_eval_linear(EvalCommon c, LinearEvalArg
       static_for<0, LIN_CH>([&](auto k) { bs1[k] = add(bs1[k], mul(b1, cur[k])); });
     }
   }
+  const felt bconst = a.coefs[4 * W], bconst1 = a.coefs[4 * W + 1];
   static_for<0, LIN_CH>([&](auto k) {
     const uint64_t q = LIN_POINT(k);
     if (q >= M) return;
@@ -933,9 +1080,9 @@ __global__ __launch_bounds__(TPB) void k_eval_linear(EvalCommon c, LinearEvalArg
     felt bnum;
     if (TWO) {
       felt e0 = sub(x, a.w_bstep), e1 = sub(x, a.w_bstep1);
-      bnum = add(mul(sub(bs0[k], a.bconst), e1), mul(sub(bs1[k], a.bconst1), e0));
+      bnum = add(mul(sub(bs0[k], bconst), e1), mul(sub(bs1[k], bconst1), e0));
     } else {
-      bnum = sub(bs0[k], a.bconst);
+      bnum = sub(bs0[k], bconst);
     }
     comp[q] = add(tpart, mul(bnum, dinv[q]));  // dinv: 1/((x - w^b0)(x - w^b1)) or 1/(x - w^b0)
   });
@@ -1311,7 +1458,8 @@ hipEvent_t Prof::get_event() {
   return e;
 }
 void Prof::begin(const char* name, hipStream_t s, double bytes) {
-  if (!enabled) return;
+  open = enabled && (only.empty() || only == name);
+  if (!open) return;
   ProfRec r;
   r.name = name;
   r.bytes = bytes;
@@ -1321,8 +1469,9 @@ void Prof::begin(const char* name, hipStream_t s, double bytes) {
   pending.push_back(r);
 }
 void Prof::end(hipStream_t s) {
-  if (!enabled) return;
+  if (!open) return;
   (void)hipEventRecord(pending.back().stop, s);
+  open = false;
 }
 
 #define LAUNCH(prof, name, stream, bytes, ...)                 \
@@ -1624,10 +1773,10 @@ void launch_grind(Prof& prof, hipStream_t s, const uint32_t* seed_words, uint64_
 }
 
 static void launch_den_inverse(Prof& prof, hipStream_t s, const PointMap& m, uint64_t count, felt c0, felt c1,
-                               int two, felt* prod) {
+                               int two, felt* prod, const felt* cdev = nullptr) {
   uint32_t nb = blocks_for((count + EVAL_CH - 1) / EVAL_CH);
   LAUNCH(prof, "den_products", s, (double)count * 16.0,
-         hipLaunchKernelGGL(k_den_products, dim3(nb), dim3(TPB), 0, s, m, count, c0, c1, two, prod));
+         hipLaunchKernelGGL(k_den_products, dim3(nb), dim3(TPB), 0, s, m, count, c0, c1, two, cdev, prod));
   LAUNCH(prof, "invert_products", s, (double)nb * 32.0,
          hipLaunchKernelGGL(k_invert_products, dim3(1), dim3(1024), 0, s, prod, nb));
 }
@@ -1679,9 +1828,9 @@ void launch_eval_bitrev(Prof& prof, hipStream_t s, const felt* arrays, uint32_t 
                             ninv, out));
 }
 
-void launch_deep_denominators(Prof& prof, hipStream_t s, const PointMap& m, uint64_t count, felt z, felt zg,
+void launch_deep_denominators(Prof& prof, hipStream_t s, const PointMap& m, uint64_t count, const felt* zz,
                               felt* binv) {
-  launch_den_inverse(prof, s, m, count, z, zg, 1, binv);
+  launch_den_inverse(prof, s, m, count, zero(), zero(), 1, binv, zz);
 }
 
 void launch_deep(Prof& prof, hipStream_t s, const DeepArgs& a, felt* out) {
@@ -1765,4 +1914,19 @@ void launch_gu_trace(Prof& prof, hipStream_t s, const felt* masked, const felt* 
   LAUNCH(prof, "gu_trace_write", s, (double)n * 2 * GU_D_DEV * 16.0 + (double)ndev * GU_D_DEV * 16.0,
          hipLaunchKernelGGL(k_gu_tile_write, dim3(tiles, 2 * GU_D_DEV), dim3(TPB), 0, s, masked, raw, local, ndev,
                             kinv, n, tile_buf, out));
+}
+
+void launch_dt_draw_coeffs(Prof& prof, hipStream_t s, uint32_t* seed, const uint32_t* root, uint32_t method,
+                           uint32_t ncoef, felt* cc) {
+  LAUNCH(prof, "coin", s, 0.0,
+         hipLaunchKernelGGL(k_dt_draw_coeffs, dim3(1), dim3(TPB), 0, s, seed, root, method, ncoef, cc));
+}
+void launch_dt_eval_consts(Prof& prof, hipStream_t s, int air, const felt* cc, felt k, const felt* aval,
+                           const felt* zinv, uint32_t ce, uint32_t w, uint32_t num_t, felt* out) {
+  LAUNCH(prof, "coin", s, 0.0,
+         hipLaunchKernelGGL(k_dt_eval_consts, dim3(1), dim3(TPB), 0, s, air, cc, k, aval, zinv, ce, w, num_t, out));
+}
+void launch_dt_draw_z(Prof& prof, hipStream_t s, uint32_t* seed, const uint32_t* root, felt wn, uint32_t logn,
+                      felt* zz, felt* pw) {
+  LAUNCH(prof, "coin", s, 0.0, hipLaunchKernelGGL(k_dt_draw_z, dim3(1), dim3(64), 0, s, seed, root, wn, logn, zz, pw));
 }

@@ -149,6 +149,21 @@ struct zkp_ctx {
   void collect_prof() {
     if (prof.pending.empty()) return;
     sync();
+    // ZKP_TIMELINE=1: per-launch (start, duration, gap to the previous launch) of
+    // this call on stderr, relative to its first launch (diagnostics only)
+    static const bool timeline = getenv("ZKP_TIMELINE") != nullptr;
+    if (timeline) {
+      const hipEvent_t t0 = prof.pending.front().start;
+      float prev_end = 0;
+      for (auto& r : prof.pending) {
+        float st = 0, en = 0;
+        (void)hipEventElapsedTime(&st, t0, r.start);
+        (void)hipEventElapsedTime(&en, t0, r.stop);
+        fprintf(stderr, "TL %-18s start %8.3f dur %7.3f gap %7.3f\n", r.name, st, en - st, st - prev_end);
+        prev_end = en;
+      }
+      fprintf(stderr, "TL end\n");
+    }
     for (auto& r : prof.pending) {
       float ms = 0;
       HIP_CHECK(hipEventElapsedTime(&ms, r.start, r.stop));
@@ -331,14 +346,18 @@ void commit_rows(zkp_ctx* ctx, zkp_comm* cm, int mode, const felt* src, uint64_t
 }
 
 // evaluate bit-reversed coefficient arrays (scaled by n) at x0, x1 -> values (x n^-1)
-void ood_eval(zkp_ctx* ctx, const felt* arrays, uint32_t narrays, uint32_t logn, felt x0, felt x1,
-              std::vector<felt>& v0, std::vector<felt>& v1) {
-  std::vector<felt> pw0(logn), pw1(logn);
-  felt a = x0, b = x1;
-  for (uint32_t l = 0; l < logn; l++) { pw0[l] = a; pw1[l] = b; a = sqr(a); b = sqr(b); }
-  felt* dpw = ctx->buf<felt>("ood_pw", 2 * (logn + 1));
-  ctx->upload(dpw, pw0.data(), logn * 16);
-  ctx->upload(dpw + logn, pw1.data(), logn * 16);
+// a device -> host copy folded into a round trip
+struct Fetch {
+  void* host;
+  const void* dev;
+  size_t bytes;
+};
+
+// OOD values of bit-reversed arrays at the two points whose power tables
+// dpw[0..logn) / dpw[logn..2logn) are in device memory; `extra` device values
+// come back in the same round trip
+void ood_eval(zkp_ctx* ctx, const felt* arrays, uint32_t narrays, uint32_t logn, const felt* dpw,
+              std::vector<felt>& v0, std::vector<felt>& v1, const std::vector<Fetch>& extra) {
   uint32_t logE = logn < 11 ? logn : 11;
   if (logn - logE > 12) throw ZkpFail{ZKP_ERR_TRACE_SHAPE, "OOD evaluation supports n <= 2^23"};
   felt* part = ctx->buf<felt>("ood_part", (size_t)2 * narrays * (1ull << (logn - logE)));
@@ -346,7 +365,24 @@ void ood_eval(zkp_ctx* ctx, const felt* arrays, uint32_t narrays, uint32_t logn,
   launch_eval_bitrev(ctx->prof, ctx->stream, arrays, narrays, logn, dpw, dpw + logn, part,
                      inv(felt_u64(1ull << logn)), dv);
   std::vector<felt> hv((size_t)2 * narrays);
-  ctx->download(hv.data(), dv, hv.size() * 16);
+  {
+    size_t tot = hv.size() * 16;
+    for (const Fetch& f : extra) tot += (f.bytes + 15) & ~(size_t)15;
+    uint8_t* hp = (uint8_t*)ctx->pinned(tot);
+    HIP_CHECK(hipMemcpyAsync(hp, dv, hv.size() * 16, hipMemcpyDeviceToHost, ctx->stream));
+    size_t o = hv.size() * 16;
+    for (const Fetch& f : extra) {
+      HIP_CHECK(hipMemcpyAsync(hp + o, f.dev, f.bytes, hipMemcpyDeviceToHost, ctx->stream));
+      o += (f.bytes + 15) & ~(size_t)15;
+    }
+    ctx->sync();
+    memcpy(hv.data(), hp, hv.size() * 16);
+    o = hv.size() * 16;
+    for (const Fetch& f : extra) {
+      memcpy(f.host, hp + o, f.bytes);
+      o += (f.bytes + 15) & ~(size_t)15;
+    }
+  }
   v0.resize(narrays);
   v1.resize(narrays);
   for (uint32_t arr = 0; arr < narrays; arr++) {
@@ -404,6 +440,24 @@ int prove_impl(zkp_ctx* ctx, zkp_comm* cm, int air_id, const felt* d_trace, uint
     se.insert(se.end(), pub.begin(), pub.end());
     coin.init(se);
   }
+  // device transcript: the coin state lives in HBM from here until
+  // the OOD download; the device draws the composition coefficients and z, the
+  // host replays both draws from the downloaded roots and checks them
+  const uint32_t ncoef = air.num_t + (uint32_t)air.a_col.size();
+  uint32_t* dt_seed = ctx->buf<uint32_t>("dt_seed", 8);
+  uint32_t* dt_roots = ctx->buf<uint32_t>("dt_roots", 16);  // staged roots of sharded commitments
+  felt* dt_cc = ctx->buf<felt>("dt_cc", ncoef);
+  felt* dt_zz = ctx->buf<felt>("dt_zz", 2);
+  felt* dt_pw = ctx->buf<felt>("dt_pw", 2 * (size_t)logn);
+  felt* dt_aval = ctx->buf<felt>("dt_aval", air.a_val.size());
+  {
+    uint32_t sw[8];
+    for (int i = 0; i < 8; i++)
+      sw[i] = (uint32_t)coin.seed[4 * i] | ((uint32_t)coin.seed[4 * i + 1] << 8) |
+              ((uint32_t)coin.seed[4 * i + 2] << 16) | ((uint32_t)coin.seed[4 * i + 3] << 24);
+    ctx->upload(dt_seed, sw, 32);
+    ctx->upload(dt_aval, air.a_val.data(), air.a_val.size() * 16);
+  }
   ctx->ensure_coset(logn, logB, logce);
   const felt* Sj0 = ctx->S(logn, logB) + (uint64_t)j0 * n;
   // domain points: coset offsets g*w_N^j (LDE cosets) and g*w_M^u (CE cosets), w_n^t table
@@ -428,14 +482,17 @@ int prove_impl(zkp_ctx* ctx, zkp_comm* cm, int air_id, const felt* d_trace, uint
     launch_ntt(pf, st, ib, logn, false, ctx->itws(logN), logN);
     NttBatch lb{coef, tlde, Sj0, n, n, Bl, Bl, w * Bl};
     launch_ntt(pf, st, lb, logn, true, ctx->tws(logN), logN);
-    commit_rows(ctx, cm, 0, tlde, n, w, logB, logn, R > 1, "ttree", ttree, T.trace_root);
+    commit_rows(ctx, cm, 0, tlde, n, w, logB, logn, R > 1, "ttree", ttree, T.trace_root, /*fetch_root=*/R > 1);
   }
-  coin.reseed(T.trace_root);
+  const uint32_t* troot_d = ttree.nodes + 8;
+  if (R > 1) {  // sharded: the root was assembled on the host from the subtree roots
+    ctx->upload(dt_roots, T.trace_root, 32);
+    troot_d = dt_roots;
+  }
   ctx->stage_end("1_trace_commit");
 
-  // 3. constraint composition coefficients + evaluation (DefaultConstraintEvaluator)
-  const uint32_t ncoef = air.num_t + (uint32_t)air.a_col.size();
-  std::vector<felt> cc = draw_coeffs(coin, o->batching_constraints, ncoef);
+  // 3. constraint composition coefficients (drawn on the device) + evaluation (DefaultConstraintEvaluator)
+  launch_dt_draw_coeffs(pf, st, dt_seed, troot_d, o->batching_constraints, ncoef, dt_cc);
   felt* comp = ctx->buf<felt>("comp", (size_t)(cel ? cel : 1) * n);
   if (cel) {
     felt wn = root_of_unity(logn);
@@ -453,15 +510,15 @@ int prove_impl(zkp_ctx* ctx, zkp_comm* cm, int air_id, const felt* d_trace, uint
       felt gn = pow_u64(g, n), wce = root_of_unity(logce);
       for (uint32_t s = 0; s < ce; s++) zinv[s] = inv(sub(mul(gn, pow_u64(wce, s)), one()));
     }
-    felt* dz = ctx->buf<felt>("zinv_coef", ce);
-    {
-      // MiMC folds its transition coefficient into the per-coset divisor constant
-      std::vector<felt> zc(zinv);
-      if (air.id == ZKP_AIR_MIMC)
-        for (auto& v : zc) v = mul(v, cc[0]);
-      ctx->upload(dz, zc.data(), ce * 16);
-    }
-    ec.zinv = dz;
+    felt* dz = ctx->buf<felt>(zkey, ce);
+    if (!ctx->have_cached(zkey)) ctx->upload(dz, zinv.data(), ce * 16);
+    // coefficient-dependent constants, built on the device from the drawn coefficients
+    // (MiMC: Z_T constants with the transition coefficient folded in, then b0, b1;
+    // linear AIRs: the 4 coefficient rows + the two boundary sums)
+    const uint32_t lw = air.id == ZKP_AIR_TRAINING_UPDATE ? w / 2 : w;
+    felt* dconst = ctx->buf<felt>("eval_consts", air.id == ZKP_AIR_MIMC ? (size_t)ce + 2 : 4 * (size_t)lw + 2);
+    launch_dt_eval_consts(pf, st, air.id, dt_cc, air.k, dt_aval, dz, ce, w, air.num_t, dconst);
+    ec.zinv = air.id == ZKP_AIR_MIMC ? dconst : dz;
     const std::string dom = std::to_string(logn) + "_" + std::to_string(logB) + "_" + std::to_string(u0) + "_" +
                             std::to_string(cel);
     if (air.id == ZKP_AIR_MIMC) {
@@ -477,9 +534,9 @@ int prove_impl(zkp_ctx* ctx, zkp_comm* cm, int air_id, const felt* d_trace, uint
         ctx->upload(dk, kv.data(), kv.size() * 16);
       }
       MimcEvalArgs ma;
-      ma.coef_t = cc[0];
-      ma.b0 = cc[1]; ma.v0 = air.a_val[0];
-      ma.b1 = cc[2]; ma.v1 = air.a_val[1];
+      ma.bcoef = dconst + ce;  // b0, b1
+      ma.v0 = air.a_val[0];
+      ma.v1 = air.a_val[1];
       ma.kper = dk;
       // divisor inverses depend only on the domain and the assertion steps: cache per config
       std::string key = "binv_mimc_" + dom;
@@ -489,27 +546,12 @@ int prove_impl(zkp_ctx* ctx, zkp_comm* cm, int air_id, const felt* d_trace, uint
       launch_eval_mimc(pf, st, ec, ma, tlde, comp);
     } else if (air.id == ZKP_AIR_GLOBAL_UPDATE) {
       // GlobalUpdate: T = sum_i a^i (k*next_i - k*cur_i - next_{i+60}); B = sum_c b_c (cur_c - v_c)
-      std::vector<felt> co(4 * w, zero());
-      for (uint32_t i = 0; i < GU_D; i++) {
-        co[i] = mul(cc[i], air.k);                    // next_i
-        co[w + i] = neg(mul(cc[i], air.k));           // cur_i
-        co[i + GU_D] = neg(cc[i]);                    // next_{i+60}
-      }
-      felt bconst = zero();
-      for (uint32_t c = 0; c < w; c++) {
-        co[2 * w + c] = cc[air.num_t + c];
-        bconst = add(bconst, mul(cc[air.num_t + c], air.a_val[c]));
-      }
-      felt* dco = ctx->buf<felt>("lin_coefs", co.size());
-      ctx->upload(dco, co.data(), co.size() * 16);
       LinearEvalArgs la;
       la.width = w;
       la.transition = true;
       la.two_groups = false;
-      la.coefs = dco;
-      la.bconst = bconst;
+      la.coefs = dconst;  // [next | cur | beta0 | beta1 | bconst0, bconst1]
       la.w_bstep = pow_u64(wn, air.a_step[0]);
-      la.bconst1 = zero();
       la.w_bstep1 = zero();
       std::string key = "binv_lin_" + dom + "_" + std::to_string(air.a_step[0]);
       la.binv_ready = ctx->have_cached(key);
@@ -520,24 +562,12 @@ int prove_impl(zkp_ctx* ctx, zkp_comm* cm, int air_id, const felt* d_trace, uint
       // TrainingUpdate: transitions identically zero; boundary groups at rows 0 and n-1 over
       // the masked columns 0..w/2 (the mask columns are never read)
       const uint32_t half = w / 2;
-      std::vector<felt> co(4 * half, zero());
-      felt bc0 = zero(), bc1 = zero();
-      for (uint32_t i = 0; i < half; i++) {
-        co[2 * half + i] = cc[air.num_t + i];
-        co[3 * half + i] = cc[air.num_t + half + i];
-        bc0 = add(bc0, mul(cc[air.num_t + i], air.a_val[i]));
-        bc1 = add(bc1, mul(cc[air.num_t + half + i], air.a_val[half + i]));
-      }
-      felt* dco = ctx->buf<felt>("lin_coefs", co.size());
-      ctx->upload(dco, co.data(), co.size() * 16);
       LinearEvalArgs la;
       la.width = half;
       la.transition = false;
       la.two_groups = true;
-      la.coefs = dco;
-      la.bconst = bc0;
+      la.coefs = dconst;
       la.w_bstep = one();
-      la.bconst1 = bc1;
       la.w_bstep1 = ec.w_last;
       std::string key = "binv_tu_" + dom;
       la.binv_ready = ctx->have_cached(key);
@@ -596,25 +626,53 @@ int prove_impl(zkp_ctx* ctx, zkp_comm* cm, int air_id, const felt* d_trace, uint
     }
     NttBatch lb{acoef, clde, Sj0, n, n, Bl, Bl, C * Bl};
     launch_ntt(pf, st, lb, logn, true, ctx->tws(logN), logN);
-    commit_rows(ctx, cm, 0, clde, n, C, logB, logn, R > 1, "ctree", ctree, T.constraint_root);
+    commit_rows(ctx, cm, 0, clde, n, C, logB, logn, R > 1, "ctree", ctree, T.constraint_root,
+                /*fetch_root=*/R > 1);
   }
-  coin.reseed(T.constraint_root);
+  const uint32_t* croot_d = ctree.nodes + 8;
+  if (R > 1) {
+    ctx->upload(dt_roots + 8, T.constraint_root, 32);
+    croot_d = dt_roots + 8;
+  }
+  const felt wn_root = root_of_unity(logn);
+  launch_dt_draw_z(pf, st, dt_seed, croot_d, wn_root, logn, dt_zz, dt_pw);
   ctx->stage_end("2_constraints_commit");
 
   // 5. OOD frame (every rank holds all trace and composition coefficients)
-  felt z = coin.draw();
-  T.z.lo = z.lo; T.z.hi = z.hi;
-  felt zg = mul(z, root_of_unity(logn));
   // the DEEP denominators (x - z)(x - zg) only need z: their batch-inversion
   // phases run on the side stream while the host finishes the OOD transcript
   felt* deep_binv = ctx->buf<felt>("binv", ((uint64_t)Bl * n) / 2048 + 1);
   const PointMap deep_pm{cx + j0, twn, logn};
   HIP_CHECK(hipEventRecord(ctx->ev_fork, st));
   HIP_CHECK(hipStreamWaitEvent(ctx->side, ctx->ev_fork, 0));
-  launch_deep_denominators(pf, ctx->side, deep_pm, (uint64_t)Bl * n, z, zg, deep_binv);
+  launch_deep_denominators(pf, ctx->side, deep_pm, (uint64_t)Bl * n, dt_zz, deep_binv);
   HIP_CHECK(hipEventRecord(ctx->ev_join, ctx->side));
   std::vector<felt> oz, ozg;
-  ood_eval(ctx, coef, w + C, logn, z, zg, oz, ozg);
+  // the first host round trip of the proof: OOD values + the device transcript so far
+  felt z, zg;
+  {
+    std::vector<felt> dcc(ncoef), dzz(2);
+    uint8_t roots[64];
+    std::vector<Fetch> extra = {{dcc.data(), dt_cc, (size_t)ncoef * 16}, {dzz.data(), dt_zz, 32},
+                                {roots, troot_d, 32}, {roots + 32, croot_d, 32}};
+    ood_eval(ctx, coef, w + C, logn, dt_pw, oz, ozg, extra);
+    memcpy(T.trace_root, roots, 32);
+    memcpy(T.constraint_root, roots + 32, 32);
+    if (R == 1) {
+      memcpy(ttree.top[1].data(), T.trace_root, 32);
+      memcpy(ctree.top[1].data(), T.constraint_root, 32);
+    }
+    // host replay of the device draws (same transcript, checked value by value)
+    coin.reseed(T.trace_root);
+    std::vector<felt> cc = draw_coeffs(coin, o->batching_constraints, ncoef);
+    coin.reseed(T.constraint_root);
+    z = coin.draw();
+    zg = mul(z, wn_root);
+    bool same = eq(z, dzz[0]) && eq(zg, dzz[1]);
+    for (uint32_t i = 0; i < ncoef && same; i++) same = eq(cc[i], dcc[i]);
+    if (!same) throw ZkpFail{ZKP_ERR_DEVICE, "device transcript diverged from the host (coefficients / z)"};
+  }
+  T.z.lo = z.lo; T.z.hi = z.hi;
   std::vector<felt> ood_trace(2 * w);
   for (uint32_t c = 0; c < w; c++) { ood_trace[c] = oz[c]; ood_trace[w + c] = ozg[c]; }
   std::vector<felt> ood_comp(oz.begin() + w, oz.end());
@@ -1291,6 +1349,13 @@ int zkp_build_global_update_trace(zkp_ctx* ctx, const zkp_felt* raw_global, cons
 int zkp_set_profiling(zkp_ctx* ctx, int enabled) {
   return guarded(ctx, [&] {
     ctx->prof.enabled = enabled != 0;
+    return 0;
+  });
+}
+
+int zkp_set_profiling_kernel(zkp_ctx* ctx, const char* kernel_name) {
+  return guarded(ctx, [&] {
+    ctx->prof.only = kernel_name ? kernel_name : "";
     return 0;
   });
 }

@@ -18,6 +18,8 @@ struct ProfRec {
 };
 struct Prof {
   bool enabled = false;
+  std::string only;   // non-empty: bracket only the launches of this name
+  bool open = false;  // the current launch is bracketed
   std::vector<ProfRec> pending;
   std::vector<hipEvent_t> pool;
   hipEvent_t get_event();
@@ -84,6 +86,18 @@ void launch_merkle_tree(Prof& prof, hipStream_t s, uint32_t* nodes, uint64_t L);
 void launch_grind(Prof& prof, hipStream_t s, const uint32_t* seed_words_dev, uint64_t base, uint64_t count,
                   uint32_t bits, unsigned long long* result);
 
+// ---------------------------------------------------------------- device transcript
+// (seed = 8 LE words of the DefaultRandomCoin state, in device memory)
+// reseed with `root` (device), then draw `ncoef` composition coefficients into cc
+void launch_dt_draw_coeffs(Prof& prof, hipStream_t s, uint32_t* seed, const uint32_t* root, uint32_t method,
+                           uint32_t ncoef, felt* cc);
+// coefficient-dependent constants of the eval kernels (layout in kernels.hip)
+void launch_dt_eval_consts(Prof& prof, hipStream_t s, int air, const felt* cc, felt k, const felt* aval,
+                           const felt* zinv, uint32_t ce, uint32_t w, uint32_t num_t, felt* out);
+// reseed with the constraint root, draw z: zz = (z, z w_n), pw = z^(2^l) || (z w_n)^(2^l), l < logn
+void launch_dt_draw_z(Prof& prof, hipStream_t s, uint32_t* seed, const uint32_t* root, felt wn, uint32_t logn,
+                      felt* zz, felt* pw);
+
 // ---------------------------------------------------------------- trace building
 // GlobalUpdate trace (120 x n, column-major) from masked/raw global models (60 each),
 // ndev x 60 local models and k^-1 (src/aggregation/prover.rs:98-160); tile_buf holds
@@ -113,7 +127,8 @@ struct EvalCommon {
 };
 // MiMC: x' - (x + K)^7 ; boundary steps 0 and n-1 on column 0
 struct MimcEvalArgs {
-  felt coef_t, b0, b1, v0, v1;
+  const felt* bcoef;     // device: b0, b1 (boundary coefficients drawn on the device)
+  felt v0, v1;
   const felt* kper;      // 64*ce periodic values on the CE domain
   felt* binv;            // scratch: one felt per 2048 CE points (per-block inverse products)
   felt* dinv;            // M felts: 1/((x - 1)(x - w^(n-1))) per CE point (domain-only, cached in the ctx)
@@ -128,9 +143,8 @@ void launch_eval_mimc(Prof& prof, hipStream_t s, const EvalCommon& c, const Mimc
 struct LinearEvalArgs {
   uint32_t width;
   bool transition, two_groups;
-  const felt* coefs;
-  felt bconst, w_bstep;
-  felt bconst1, w_bstep1;
+  const felt* coefs;     // device: 4 * width coefficient rows, then bconst0, bconst1
+  felt w_bstep, w_bstep1;
   felt* binv;            // scratch: one felt per 2048 CE points
   felt* dinv;            // M felts: the boundary divisor inverses per CE point (cached in the ctx)
   bool binv_ready;       // dinv already holds this domain's values
@@ -161,7 +175,7 @@ struct DeepArgs {
 };
 // phases 1-2 of the DEEP batch inversion (block inverse products of (x - z)(x - zg)
 // into binv); launch_deep then runs phase 3 + the composition
-void launch_deep_denominators(Prof& prof, hipStream_t s, const PointMap& m, uint64_t count, felt z, felt zg,
+void launch_deep_denominators(Prof& prof, hipStream_t s, const PointMap& m, uint64_t count, const felt* zz,
                               felt* binv);
 void launch_deep(Prof& prof, hipStream_t s, const DeepArgs& a, felt* out);
 
