@@ -694,6 +694,139 @@ __device__ __forceinline__ felt dcoin_draw(const uint32_t s[8], uint64_t* ctr) {
   return fp::zero();
 }
 
+// draw `ncoef` coefficients into out (whole block; the coin state s was just
+// reseeded, counter 0): Linear = ncoef draws (parallel candidates, sequential redo
+// on a rejection), Algebraic = powers of one draw, Horner = the powers reversed
+__device__ void dcoin_draw_coeffs_block(const uint32_t s[8], uint32_t method, uint32_t ncoef, felt* out,
+                                        felt* s_alpha, int* s_rej) {
+  if (threadIdx.x == 0) {
+    *s_rej = 0;
+    if (method != ZKP_BATCHING_LINEAR) {
+      uint64_t ctr = 0;
+      *s_alpha = dcoin_draw(s, &ctr);
+    }
+  }
+  __syncthreads();
+  if (method == ZKP_BATCHING_LINEAR) {
+    for (uint32_t i = threadIdx.x; i < ncoef; i += blockDim.x) {
+      felt v = dcoin_candidate(s, (uint64_t)i + 1);
+      if (fp::ge_p(v)) *s_rej = 1;
+      out[i] = v;
+    }
+    __syncthreads();
+    if (*s_rej && threadIdx.x == 0) {
+      uint64_t ctr = 0;
+      for (uint32_t i = 0; i < ncoef; i++) out[i] = dcoin_draw(s, &ctr);
+    }
+    __syncthreads();
+    return;
+  }
+  const felt a = *s_alpha;
+  for (uint32_t i = threadIdx.x; i < ncoef; i += blockDim.x)
+    out[method == ZKP_BATCHING_HORNER ? ncoef - 1 - i : i] = fp::pow_u64(a, i);
+  __syncthreads();
+}
+
+// Blake3_256::hash_elements over nf felts get(i) by a whole block: chunk c
+// (64 felts) on thread c, then the chunk tree (left subtree = largest power of
+// two) on thread 0 with the incremental stack. nf <= 64 * 32.
+template <typename Get>
+__device__ void hash_felts_block(Get get, uint32_t nf, uint32_t out[8], uint32_t (*s_cv)[8]) {
+  const uint32_t nch = nf ? (nf + 63) / 64 : 1;
+  for (uint32_t c = threadIdx.x; c < nch; c += blockDim.x) {
+    uint32_t cv[8];
+    const uint32_t f0 = 64 * c, f1 = f0 + 64 < nf ? f0 + 64 : nf;
+    b3::hash_chunk(get, f0, f1, c, nch == 1, cv);
+    for (int i = 0; i < 8; i++) s_cv[c][i] = cv[i];
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    if (nch == 1) {
+      for (int i = 0; i < 8; i++) out[i] = s_cv[0][i];
+    } else {
+      uint32_t st[6][8];
+      int top = 0;
+      for (uint32_t c = 0; c + 1 < nch; c++) {
+        uint32_t cv[8];
+        for (int i = 0; i < 8; i++) cv[i] = s_cv[c][i];
+        uint64_t total = c + 1;
+        while ((total & 1) == 0) {
+          uint32_t p[8];
+          b3::parent(st[--top], cv, false, p);
+          for (int i = 0; i < 8; i++) cv[i] = p[i];
+          total >>= 1;
+        }
+        for (int i = 0; i < 8; i++) st[top][i] = cv[i];
+        top++;
+      }
+      uint32_t cv[8];
+      for (int i = 0; i < 8; i++) cv[i] = s_cv[nch - 1][i];
+      while (top > 0) {
+        uint32_t p[8];
+        top--;
+        b3::parent(st[top], cv, top == 0, p);
+        for (int i = 0; i < 8; i++) cv[i] = p[i];
+      }
+      for (int i = 0; i < 8; i++) out[i] = cv[i];
+    }
+  }
+  __syncthreads();
+}
+
+// OOD frame -> transcript -> DEEP coefficients, on the device: reseed with
+// H(T(z) || T(zg)) and H(H_j(z)), draw the w + C DEEP coefficients, and the
+// constants kz = sum gamma_i T_i(z) + sum gamma_j H_j(z), kzg = sum gamma_i T_i(zg).
+// ood[2a + {0,1}] = array a at (z, zg), arrays = w trace columns then C composition columns.
+// dk = [z, zg] on entry; [z, zg, kz, kzg] on exit.
+__global__ __launch_bounds__(64) void k_dt_deep_coeffs(uint32_t* __restrict__ seed, const felt* __restrict__ ood,
+                                                       uint32_t w, uint32_t C, uint32_t method,
+                                                       felt* __restrict__ gamma, felt* __restrict__ dk) {
+  __shared__ uint32_t s_cv[32][8];
+  __shared__ uint32_t s[8];
+  __shared__ felt s_alpha;
+  __shared__ int s_rej;
+  __shared__ felt red0[64], red1[64];
+  uint32_t h[8];
+  hash_felts_block([&](uint32_t i) { return i < w ? ood[2 * i] : ood[2 * (i - w) + 1]; }, 2 * w, h, s_cv);
+  if (threadIdx.x == 0) {
+    uint32_t t[8];
+    for (int i = 0; i < 8; i++) t[i] = seed[i];
+    dcoin_reseed(t, h);
+    for (int i = 0; i < 8; i++) s[i] = t[i];
+  }
+  __syncthreads();
+  hash_felts_block([&](uint32_t i) { return ood[2 * (w + i)]; }, C, h, s_cv);
+  if (threadIdx.x == 0) {
+    uint32_t t[8];
+    for (int i = 0; i < 8; i++) t[i] = s[i];
+    dcoin_reseed(t, h);
+    for (int i = 0; i < 8; i++) { s[i] = t[i]; seed[i] = t[i]; }
+  }
+  __syncthreads();
+  uint32_t t[8];
+  for (int i = 0; i < 8; i++) t[i] = s[i];
+  dcoin_draw_coeffs_block(t, method, w + C, gamma, &s_alpha, &s_rej);
+  felt a = zero(), b = zero();
+  for (uint32_t i = threadIdx.x; i < w + C; i += blockDim.x) {
+    a = add(a, mul(gamma[i], ood[2 * i]));
+    if (i < w) b = add(b, mul(gamma[i], ood[2 * i + 1]));
+  }
+  red0[threadIdx.x] = a;
+  red1[threadIdx.x] = b;
+  __syncthreads();
+  for (uint32_t k = 32; k >= 1; k >>= 1) {
+    if (threadIdx.x < k) {
+      red0[threadIdx.x] = add(red0[threadIdx.x], red0[threadIdx.x + k]);
+      red1[threadIdx.x] = add(red1[threadIdx.x], red1[threadIdx.x + k]);
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    dk[2] = red0[0];
+    dk[3] = red1[0];
+  }
+}
+
 // reseed with the trace root, then the constraint composition coefficients
 // (ConstraintCompositionCoefficients::draw: Linear = n draws, Algebraic = powers
 // of one draw, Horner = the powers reversed). One block; Linear draws run in
@@ -701,38 +834,18 @@ __device__ __forceinline__ felt dcoin_draw(const uint32_t s[8], uint64_t* ctr) {
 __global__ __launch_bounds__(TPB) void k_dt_draw_coeffs(uint32_t* __restrict__ seed, const uint32_t* __restrict__ root,
                                                         uint32_t method, uint32_t ncoef, felt* __restrict__ cc) {
   __shared__ uint32_t s[8];
-  __shared__ felt alpha;
-  __shared__ int rejected;
+  __shared__ felt s_alpha;
+  __shared__ int s_rej;
   if (threadIdx.x == 0) {
     uint32_t t[8], d[8];
     for (int i = 0; i < 8; i++) { t[i] = seed[i]; d[i] = root[i]; }
     dcoin_reseed(t, d);
     for (int i = 0; i < 8; i++) { s[i] = t[i]; seed[i] = t[i]; }
-    rejected = 0;
-    if (method != ZKP_BATCHING_LINEAR) {
-      uint64_t ctr = 0;
-      alpha = dcoin_draw(t, &ctr);
-    }
   }
   __syncthreads();
   uint32_t t[8];
   for (int i = 0; i < 8; i++) t[i] = s[i];
-  if (method == ZKP_BATCHING_LINEAR) {
-    for (uint32_t i = threadIdx.x; i < ncoef; i += TPB) {
-      felt v = dcoin_candidate(t, (uint64_t)i + 1);
-      if (fp::ge_p(v)) rejected = 1;
-      cc[i] = v;
-    }
-    __syncthreads();
-    if (rejected && threadIdx.x == 0) {  // probability ~2^-82 per draw: redo sequentially
-      uint64_t ctr = 0;
-      for (uint32_t i = 0; i < ncoef; i++) cc[i] = dcoin_draw(t, &ctr);
-    }
-    return;
-  }
-  const felt a = alpha;
-  for (uint32_t i = threadIdx.x; i < ncoef; i += TPB)
-    cc[method == ZKP_BATCHING_HORNER ? ncoef - 1 - i : i] = fp::pow_u64(a, i);
+  dcoin_draw_coeffs_block(t, method, ncoef, cc, &s_alpha, &s_rej);
 }
 
 // coefficient-dependent constants of the constraint evaluation kernels, from cc:
@@ -1204,6 +1317,7 @@ __global__ __launch_bounds__(TPB) void k_eval_bitrev_tail(const felt* __restrict
 // the LDE matrices are read at offset q (contiguous), output is coset-major.
 __global__ __launch_bounds__(TPB) void k_deep(DeepArgs a, const felt* __restrict__ binv, felt* __restrict__ out) {
   __shared__ felt s_pre[TPB], s_suf[TPB];
+  const felt z = a.dk[0], zg = a.dk[1], kz = a.dk[2], kzg = a.dk[3];
   const uint64_t N = 1ull << (a.logn + a.logBl);
   const uint64_t cstride = N;
   felt A[EVAL_CH], Bh[EVAL_CH];
@@ -1234,8 +1348,8 @@ __global__ __launch_bounds__(TPB) void k_deep(DeepArgs a, const felt* __restrict
   static_for<0, EVAL_CH>([&](auto k) {
     const bool valid = EVAL_POINT(k) < N;
     felt x = point_x(a.pm, off[k]);
-    felt e1 = sub(x, a.z), e2 = sub(x, a.zg);
-    num[k] = add(mul(sub(add(A[k], Bh[k]), a.kz), e2), mul(sub(A[k], a.kzg), e1));
+    felt e1 = sub(x, z), e2 = sub(x, zg);
+    num[k] = add(mul(sub(add(A[k], Bh[k]), kz), e2), mul(sub(A[k], kzg), e1));
     den[k] = valid ? mul(e1, e2) : one();
   });
   block_batch_inverse(den, s_pre, s_suf, binv[blockIdx.x]);
@@ -1929,4 +2043,10 @@ void launch_dt_eval_consts(Prof& prof, hipStream_t s, int air, const felt* cc, f
 void launch_dt_draw_z(Prof& prof, hipStream_t s, uint32_t* seed, const uint32_t* root, felt wn, uint32_t logn,
                       felt* zz, felt* pw) {
   LAUNCH(prof, "coin", s, 0.0, hipLaunchKernelGGL(k_dt_draw_z, dim3(1), dim3(64), 0, s, seed, root, wn, logn, zz, pw));
+}
+
+void launch_dt_deep_coeffs(Prof& prof, hipStream_t s, uint32_t* seed, const felt* ood, uint32_t w, uint32_t C,
+                           uint32_t method, felt* gamma, felt* dk) {
+  LAUNCH(prof, "coin", s, 0.0,
+         hipLaunchKernelGGL(k_dt_deep_coeffs, dim3(1), dim3(64), 0, s, seed, ood, w, C, method, gamma, dk));
 }

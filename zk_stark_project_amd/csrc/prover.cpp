@@ -353,42 +353,35 @@ struct Fetch {
   size_t bytes;
 };
 
+// device -> host copies of one round trip (one sync)
+void fetch_all(zkp_ctx* ctx, const std::vector<Fetch>& fs) {
+  size_t tot = 0;
+  for (const Fetch& f : fs) tot += (f.bytes + 15) & ~(size_t)15;
+  uint8_t* hp = (uint8_t*)ctx->pinned(tot + 16);
+  size_t o = 0;
+  for (const Fetch& f : fs) {
+    if (f.bytes) HIP_CHECK(hipMemcpyAsync(hp + o, f.dev, f.bytes, hipMemcpyDeviceToHost, ctx->stream));
+    o += (f.bytes + 15) & ~(size_t)15;
+  }
+  ctx->sync();
+  o = 0;
+  for (const Fetch& f : fs) {
+    memcpy(f.host, hp + o, f.bytes);
+    o += (f.bytes + 15) & ~(size_t)15;
+  }
+}
+
 // OOD values of bit-reversed arrays at the two points whose power tables
-// dpw[0..logn) / dpw[logn..2logn) are in device memory; `extra` device values
-// come back in the same round trip
-void ood_eval(zkp_ctx* ctx, const felt* arrays, uint32_t narrays, uint32_t logn, const felt* dpw,
-              std::vector<felt>& v0, std::vector<felt>& v1, const std::vector<Fetch>& extra) {
+// dpw[0..logn) / dpw[logn..2logn) are in device memory; returns the device
+// array ood[2a + {0,1}] (array a at the two points)
+felt* ood_launch(zkp_ctx* ctx, const felt* arrays, uint32_t narrays, uint32_t logn, const felt* dpw) {
   uint32_t logE = logn < 11 ? logn : 11;
   if (logn - logE > 12) throw ZkpFail{ZKP_ERR_TRACE_SHAPE, "OOD evaluation supports n <= 2^23"};
   felt* part = ctx->buf<felt>("ood_part", (size_t)2 * narrays * (1ull << (logn - logE)));
   felt* dv = ctx->buf<felt>("ood_vals", (size_t)2 * narrays);
   launch_eval_bitrev(ctx->prof, ctx->stream, arrays, narrays, logn, dpw, dpw + logn, part,
                      inv(felt_u64(1ull << logn)), dv);
-  std::vector<felt> hv((size_t)2 * narrays);
-  {
-    size_t tot = hv.size() * 16;
-    for (const Fetch& f : extra) tot += (f.bytes + 15) & ~(size_t)15;
-    uint8_t* hp = (uint8_t*)ctx->pinned(tot);
-    HIP_CHECK(hipMemcpyAsync(hp, dv, hv.size() * 16, hipMemcpyDeviceToHost, ctx->stream));
-    size_t o = hv.size() * 16;
-    for (const Fetch& f : extra) {
-      HIP_CHECK(hipMemcpyAsync(hp + o, f.dev, f.bytes, hipMemcpyDeviceToHost, ctx->stream));
-      o += (f.bytes + 15) & ~(size_t)15;
-    }
-    ctx->sync();
-    memcpy(hv.data(), hp, hv.size() * 16);
-    o = hv.size() * 16;
-    for (const Fetch& f : extra) {
-      memcpy(f.host, hp + o, f.bytes);
-      o += (f.bytes + 15) & ~(size_t)15;
-    }
-  }
-  v0.resize(narrays);
-  v1.resize(narrays);
-  for (uint32_t arr = 0; arr < narrays; arr++) {
-    v0[arr] = hv[2 * arr];
-    v1[arr] = hv[2 * arr + 1];
-  }
+  return dv;
 }
 
 int prove_impl(zkp_ctx* ctx, zkp_comm* cm, int air_id, const felt* d_trace, uint32_t w, uint64_t n,
@@ -647,62 +640,30 @@ int prove_impl(zkp_ctx* ctx, zkp_comm* cm, int air_id, const felt* d_trace, uint
   HIP_CHECK(hipStreamWaitEvent(ctx->side, ctx->ev_fork, 0));
   launch_deep_denominators(pf, ctx->side, deep_pm, (uint64_t)Bl * n, dt_zz, deep_binv);
   HIP_CHECK(hipEventRecord(ctx->ev_join, ctx->side));
-  std::vector<felt> oz, ozg;
-  // the first host round trip of the proof: OOD values + the device transcript so far
-  felt z, zg;
-  {
-    std::vector<felt> dcc(ncoef), dzz(2);
-    uint8_t roots[64];
-    std::vector<Fetch> extra = {{dcc.data(), dt_cc, (size_t)ncoef * 16}, {dzz.data(), dt_zz, 32},
-                                {roots, troot_d, 32}, {roots + 32, croot_d, 32}};
-    ood_eval(ctx, coef, w + C, logn, dt_pw, oz, ozg, extra);
-    memcpy(T.trace_root, roots, 32);
-    memcpy(T.constraint_root, roots + 32, 32);
-    if (R == 1) {
-      memcpy(ttree.top[1].data(), T.trace_root, 32);
-      memcpy(ctree.top[1].data(), T.constraint_root, 32);
-    }
-    // host replay of the device draws (same transcript, checked value by value)
-    coin.reseed(T.trace_root);
-    std::vector<felt> cc = draw_coeffs(coin, o->batching_constraints, ncoef);
-    coin.reseed(T.constraint_root);
-    z = coin.draw();
-    zg = mul(z, wn_root);
-    bool same = eq(z, dzz[0]) && eq(zg, dzz[1]);
-    for (uint32_t i = 0; i < ncoef && same; i++) same = eq(cc[i], dcc[i]);
-    if (!same) throw ZkpFail{ZKP_ERR_DEVICE, "device transcript diverged from the host (coefficients / z)"};
-  }
-  T.z.lo = z.lo; T.z.hi = z.hi;
-  std::vector<felt> ood_trace(2 * w);
-  for (uint32_t c = 0; c < w; c++) { ood_trace[c] = oz[c]; ood_trace[w + c] = ozg[c]; }
-  std::vector<felt> ood_comp(oz.begin() + w, oz.end());
-  uint8_t dg[32];
-  hash_elements(ood_trace.data(), ood_trace.size(), dg);
-  coin.reseed(dg);
-  hash_elements(ood_comp.data(), ood_comp.size(), dg);
-  coin.reseed(dg);
+  // OOD frame and DEEP coefficients on the device (device transcript); the host
+  // replays both at the FRI round trip
+  felt* dv = ood_launch(ctx, coef, w + C, logn, dt_pw);
+  felt* dgam = ctx->buf<felt>("gamma", w + C);
+  felt* dk = ctx->buf<felt>("dt_dk", 4);
+  HIP_CHECK(hipMemcpyAsync(dk, dt_zz, 32, hipMemcpyDeviceToDevice, st));
+  launch_dt_deep_coeffs(pf, st, dt_seed, dv, w, C, o->batching_deep, dgam, dk);
   ctx->stage_end("3_ood");
 
   // 6. DEEP composition evaluations over this rank's cosets (coset-major)
-  std::vector<felt> gam = draw_coeffs(coin, o->batching_deep, w + C);
   felt* deep = ctx->buf<felt>("deep", (size_t)Bl * n);
   {
-    felt kz = zero(), kzg = zero();
-    for (uint32_t c = 0; c < w; c++) { kz = add(kz, mul(gam[c], oz[c])); kzg = add(kzg, mul(gam[c], ozg[c])); }
-    for (uint32_t h = 0; h < C; h++) kz = add(kz, mul(gam[w + h], oz[w + h]));
-    felt* dg2 = ctx->buf<felt>("gamma", w + C);
-    ctx->upload(dg2, gam.data(), gam.size() * 16);
     DeepArgs da;
     da.w = w; da.C = C; da.logB = logB; da.logn = logn; da.logN = logN;
     da.j0 = j0; da.logBl = logBl;
-    da.tlde = tlde; da.clde = clde; da.gamma = dg2;
-    da.z = z; da.zg = zg; da.kz = kz; da.kzg = kzg; da.g = g;
+    da.tlde = tlde; da.clde = clde; da.gamma = dgam; da.dk = dk; da.g = g;
     da.pm = deep_pm;
     da.binv = deep_binv;
     HIP_CHECK(hipStreamWaitEvent(st, ctx->ev_join, 0));
     launch_deep(pf, st, da, deep);
   }
   ctx->stage_end("4_deep_launch");
+
+  std::vector<felt> ood_trace(2 * (size_t)w), ood_comp(C);  // filled by the host replay below
 
   // 7. FRI layers (FriProver::build_layers), folding factor 16. Layers stay
   // coset-sharded while each rank's Merkle range has >= 16 rows per coset,
@@ -751,13 +712,7 @@ int prove_impl(zkp_ctx* ctx, zkp_comm* cm, int air_id, const felt* d_trace, uint
     uint32_t* coin_d = ctx->buf<uint32_t>("fri_coin", 8 + 12 * (size_t)(L + 1));
     felt* alphas_d = reinterpret_cast<felt*>(coin_d + 8);
     uint32_t* roots_d = coin_d + 8 + 4 * (size_t)L;
-    {
-      uint32_t sw[8];
-      for (int i = 0; i < 8; i++)
-        sw[i] = (uint32_t)coin.seed[4 * i] | ((uint32_t)coin.seed[4 * i + 1] << 8) |
-                ((uint32_t)coin.seed[4 * i + 2] << 16) | ((uint32_t)coin.seed[4 * i + 3] << 24);
-      ctx->upload(coin_d, sw, 32);
-    }
+    HIP_CHECK(hipMemcpyAsync(coin_d, dt_seed, 32, hipMemcpyDeviceToDevice, st));  // device transcript
     for (uint32_t l = 0; l < L; l++) {
       const uint64_t m16 = m / F;
       if (sh && (m16 >> logR) < 16) replicate(l);
@@ -784,22 +739,48 @@ int prove_impl(zkp_ctx* ctx, zkp_comm* cm, int air_id, const felt* d_trace, uint
     }
     if (sh) replicate(L);
     layers[L].E = E; layers[L].m = m; layers[L].Bc = B; layers[L].jc = 0; layers[L].sharded = false;
-    // one round trip: roots + device alphas + the last layer
+    // the proof's first host round trip: the device transcript so far (commitment
+    // roots, coefficients, z, OOD frame, DEEP coefficients, FRI roots + alphas)
+    // and the last FRI layer
     std::vector<uint8_t> rb((size_t)L * 32);
     std::vector<felt> dalpha(L);
     std::vector<felt> cm_vals((size_t)B * m);
-    {
-      size_t ab = (size_t)L * 16, rbb = (size_t)L * 32, lb = cm_vals.size() * 16;
-      uint8_t* hp = (uint8_t*)ctx->pinned(ab + rbb + lb + 64);
-      if (L) {
-        HIP_CHECK(hipMemcpyAsync(hp, alphas_d, ab + rbb, hipMemcpyDeviceToHost, st));
-      }
-      HIP_CHECK(hipMemcpyAsync(hp + ab + rbb, E, lb, hipMemcpyDeviceToHost, st));
-      ctx->sync();
-      memcpy(dalpha.data(), hp, ab);
-      memcpy(rb.data(), hp + ab, rbb);
-      memcpy(cm_vals.data(), hp + ab + rbb, lb);
+    std::vector<felt> dcc(ncoef), dzz(2), hood((size_t)2 * (w + C)), hgam(w + C), hdk(4);
+    uint8_t roots[64];
+    fetch_all(ctx, {{dalpha.data(), alphas_d, (size_t)L * 16}, {rb.data(), roots_d, (size_t)L * 32},
+                    {cm_vals.data(), E, cm_vals.size() * 16}, {dcc.data(), dt_cc, (size_t)ncoef * 16},
+                    {dzz.data(), dt_zz, 32}, {hood.data(), dv, hood.size() * 16},
+                    {hgam.data(), dgam, hgam.size() * 16}, {hdk.data(), dk, 64},
+                    {roots, troot_d, 32}, {roots + 32, croot_d, 32}});
+    memcpy(T.trace_root, roots, 32);
+    memcpy(T.constraint_root, roots + 32, 32);
+    if (R == 1) {
+      memcpy(ttree.top[1].data(), T.trace_root, 32);
+      memcpy(ctree.top[1].data(), T.constraint_root, 32);
     }
+    // host replay of the device transcript, checked value by value
+    bool same = true;
+    coin.reseed(T.trace_root);
+    std::vector<felt> cc = draw_coeffs(coin, o->batching_constraints, ncoef);
+    for (uint32_t i = 0; i < ncoef && same; i++) same = eq(cc[i], dcc[i]);
+    coin.reseed(T.constraint_root);
+    const felt z = coin.draw(), zg = mul(z, wn_root);
+    same = same && eq(z, dzz[0]) && eq(zg, dzz[1]);
+    T.z.lo = z.lo; T.z.hi = z.hi;
+    for (uint32_t c = 0; c < w; c++) { ood_trace[c] = hood[2 * c]; ood_trace[w + c] = hood[2 * c + 1]; }
+    for (uint32_t h = 0; h < C; h++) ood_comp[h] = hood[2 * (w + h)];
+    uint8_t dg[32];
+    hash_elements(ood_trace.data(), ood_trace.size(), dg);
+    coin.reseed(dg);
+    hash_elements(ood_comp.data(), ood_comp.size(), dg);
+    coin.reseed(dg);
+    std::vector<felt> gam = draw_coeffs(coin, o->batching_deep, w + C);
+    felt kz = zero(), kzg = zero();
+    for (uint32_t c = 0; c < w; c++) { kz = add(kz, mul(gam[c], ood_trace[c])); kzg = add(kzg, mul(gam[c], ood_trace[w + c])); }
+    for (uint32_t h = 0; h < C; h++) kz = add(kz, mul(gam[w + h], ood_comp[h]));
+    for (uint32_t i = 0; i < w + C && same; i++) same = eq(gam[i], hgam[i]);
+    same = same && eq(kz, hdk[2]) && eq(kzg, hdk[3]);
+    if (!same) throw ZkpFail{ZKP_ERR_DEVICE, "device transcript diverged from the host (coefficients / z / DEEP)"};
     // host transcript replay (the proof's commitments and the coin state)
     for (uint32_t l = 0; l < L; l++) {
       memcpy(T.fri_roots[l], rb.data() + 32 * (size_t)l, 32);

@@ -94,6 +94,10 @@ void launch_dt_draw_coeffs(Prof& prof, hipStream_t s, uint32_t* seed, const uint
 // coefficient-dependent constants of the eval kernels (layout in kernels.hip)
 void launch_dt_eval_consts(Prof& prof, hipStream_t s, int air, const felt* cc, felt k, const felt* aval,
                            const felt* zinv, uint32_t ce, uint32_t w, uint32_t num_t, felt* out);
+// OOD frame -> reseeds -> DEEP coefficients gamma (w + C) and dk[2..4) = kz, kzg
+// (ood[2a + {0,1}] = array a at z, zg; dk[0..2) = z, zg already)
+void launch_dt_deep_coeffs(Prof& prof, hipStream_t s, uint32_t* seed, const felt* ood, uint32_t w, uint32_t C,
+                           uint32_t method, felt* gamma, felt* dk);
 // reseed with the constraint root, draw z: zz = (z, z w_n), pw = z^(2^l) || (z w_n)^(2^l), l < logn
 void launch_dt_draw_z(Prof& prof, hipStream_t s, uint32_t* seed, const uint32_t* root, felt wn, uint32_t logn,
                       felt* zz, felt* pw);
@@ -169,7 +173,8 @@ struct DeepArgs {
   const felt* tlde;      // w x Bl x n
   const felt* clde;      // C x Bl x n
   const felt* gamma;     // w + C
-  felt z, zg, kz, kzg, g;
+  const felt* dk;        // device: z, z*w_n, kz, kzg (drawn / formed on the device)
+  felt g;
   PointMap pm;           // x of the shard's LDE points (cx per owned coset)
   felt* binv;            // scratch: one felt per 2048 LDE points
 };
