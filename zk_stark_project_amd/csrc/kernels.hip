@@ -181,6 +181,14 @@ __device__ __forceinline__ void bfly(felt& x, felt& y, felt w) {
 #define ZKP_EXP_NOBFLY_ON false
 #endif
 
+// butterfly with twiddle 1 (no product)
+template <bool DIT>
+__device__ __forceinline__ void bfly1(felt& x, felt& y) {
+  felt d = sub(x, y);
+  x = add(x, y);
+  y = d;
+}
+
 // rounds of a K-stage pass: <= 3 stages each, larger first
 template <int K>
 struct NttRounds {
@@ -219,7 +227,11 @@ __device__ __forceinline__ void bfly2(felt& x0, felt& y0, felt w0, felt& x1, fel
 #endif
 }
 
-template <bool DIT, int NT, int KC>
+// SMALL: this pass holds the transform's smallest stages 0..2 (DIT first pass /
+// DIF last pass, lo = 0); its round over them has jb = 0, so every twiddle of
+// stage 0, half of stage 1 and a quarter of stage 2 is 1 and those products are
+// skipped. A template flag, so the other passes keep their register budget.
+template <bool DIT, int NT, int KC, bool SMALL>
 __global__ __launch_bounds__(NT) void k_ntt8(Ntt8Args a) {
   constexpr int E = NT * 8;
   extern __shared__ felt lds[];
@@ -324,7 +336,27 @@ __global__ __launch_bounds__(NT) void k_ntt8(Ntt8Args a) {
       const uint64_t l = l0 + (ggs[0] & (Tl - 1));
       const uint64_t jb = ((uint64_t)qlow[0] << lo) | l;
       const uint64_t jstep = 1ull << (b0 + lo);
-      if (DIT) {
+      // stages 0..2 (b0 = 0, lo = 0, so jb = 0): 7 of the 12 products are by 1
+      constexpr bool smallest = SMALL && (DIT ? first : last);
+      if constexpr (DIT && smallest) {
+        bfly1<true>(x[0], x[1]); bfly1<true>(x[2], x[3]); bfly1<true>(x[4], x[5]); bfly1<true>(x[6], x[7]);
+        const felt w1 = ntt_tw<true>(a, 1, 1);
+        bfly1<true>(x[0], x[2]); bfly1<true>(x[4], x[6]);
+        bfly2<true>(x[1], x[3], w1, x[5], x[7], w1);
+        const felt w21 = ntt_tw<true>(a, 1, 2), w22 = ntt_tw<true>(a, 2, 2), w23 = ntt_tw<true>(a, 3, 2);
+        bfly1<true>(x[0], x[4]);
+        bfly2<true>(x[1], x[5], w21, x[2], x[6], w22);
+        bfly<true>(x[3], x[7], w23);
+      } else if constexpr (!DIT && smallest) {
+        const felt w21 = ntt_tw<false>(a, 1, 2), w22 = ntt_tw<false>(a, 2, 2), w23 = ntt_tw<false>(a, 3, 2);
+        bfly1<false>(x[0], x[4]);
+        bfly2<false>(x[1], x[5], w21, x[2], x[6], w22);
+        bfly<false>(x[3], x[7], w23);
+        const felt w1 = ntt_tw<false>(a, 1, 1);
+        bfly1<false>(x[0], x[2]); bfly1<false>(x[4], x[6]);
+        bfly2<false>(x[1], x[3], w1, x[5], x[7], w1);
+        bfly1<false>(x[0], x[1]); bfly1<false>(x[2], x[3]); bfly1<false>(x[4], x[5]); bfly1<false>(x[6], x[7]);
+      } else if constexpr (DIT) {
         {
           felt w0 = ntt_tw<true>(a, jb, b0);
           bfly2<true>(x[0], x[1], w0, x[2], x[3], w0); bfly2<true>(x[4], x[5], w0, x[6], x[7], w0);
@@ -356,6 +388,16 @@ __global__ __launch_bounds__(NT) void k_ntt8(Ntt8Args a) {
         }
       }
     } else if constexpr (rb == 2 && !ZKP_EXP_NOBFLY_ON) {
+      if constexpr (!DIT && SMALL && last) {  // DIF stages 1, 0: one product of four is not by 1
+        const felt w1 = ntt_tw<false>(a, 1, 1);
+#pragma unroll
+        for (int u = 0; u < 2; u++) {
+          felt* y = x + 4 * u;
+          bfly1<false>(y[0], y[2]);
+          bfly<false>(y[1], y[3], w1);
+          bfly1<false>(y[0], y[1]); bfly1<false>(y[2], y[3]);
+        }
+      } else {
 #pragma unroll
       for (int u = 0; u < 2; u++) {
         const uint64_t l = l0 + (ggs[u] & (Tl - 1));
@@ -370,6 +412,7 @@ __global__ __launch_bounds__(NT) void k_ntt8(Ntt8Args a) {
           bfly2<false>(y[0], y[2], w1a, y[1], y[3], w1b);
           bfly2<false>(y[0], y[1], w0, y[2], y[3], w0);
         }
+      }
       }
     } else if constexpr (!ZKP_EXP_NOBFLY_ON) {
 #pragma unroll
@@ -1681,10 +1724,15 @@ void launch_ntt(Prof& prof, hipStream_t s, const NttBatch& b, uint32_t logn, boo
   static bool attr_set = false;
   if (!attr_set) {
     size_t maxb = (size_t)(1u << LOGE) * sizeof(felt);
-    const void* fns[] = {(const void*)k_ntt8<true, 256, 5>, (const void*)k_ntt8<true, 256, 6>,
-                         (const void*)k_ntt8<true, 256, 7>, (const void*)k_ntt8<true, 256, 8>,
-                         (const void*)k_ntt8<false, 256, 5>, (const void*)k_ntt8<false, 256, 6>,
-                         (const void*)k_ntt8<false, 256, 7>, (const void*)k_ntt8<false, 256, 8>};
+    const void* fns[] = {
+        (const void*)k_ntt8<true, 256, 5, false>,  (const void*)k_ntt8<true, 256, 6, false>,
+        (const void*)k_ntt8<true, 256, 7, false>,  (const void*)k_ntt8<true, 256, 8, false>,
+        (const void*)k_ntt8<false, 256, 5, false>, (const void*)k_ntt8<false, 256, 6, false>,
+        (const void*)k_ntt8<false, 256, 7, false>, (const void*)k_ntt8<false, 256, 8, false>,
+        (const void*)k_ntt8<true, 256, 5, true>,   (const void*)k_ntt8<true, 256, 6, true>,
+        (const void*)k_ntt8<true, 256, 7, true>,   (const void*)k_ntt8<true, 256, 8, true>,
+        (const void*)k_ntt8<false, 256, 5, true>,  (const void*)k_ntt8<false, 256, 6, true>,
+        (const void*)k_ntt8<false, 256, 7, true>,  (const void*)k_ntt8<false, 256, 8, true>};
     for (const void* f : fns) (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)maxb);
     attr_set = true;
   }
@@ -1743,9 +1791,12 @@ void launch_ntt(Prof& prof, hipStream_t s, const NttBatch& b, uint32_t logn, boo
     const uint32_t src_arrays = first ? (b.batches + a.src_div - 1) / a.src_div : b.batches;
     const uint32_t scale_rows = a.scale ? (a.scale_mod < b.batches ? a.scale_mod : b.batches) : 0;
     const double bytes = arr * ((double)src_arrays + scale_rows + b.batches);
+    // the pass over stages 0..2 (lo = 0): the trivial-twiddle variant
+    const bool small = a.lo == 0;
 #define ZKP_NTT8(D, KK)                                                                                  \
   LAUNCH(prof, D ? "ntt_dit" : "ntt_dif", s, bytes,                                                     \
-         hipLaunchKernelGGL((k_ntt8<D, 256, KK>), grid, dim3(256), shmem, s, a))
+         if (small) hipLaunchKernelGGL((k_ntt8<D, 256, KK, true>), grid, dim3(256), shmem, s, a);         \
+         else hipLaunchKernelGGL((k_ntt8<D, 256, KK, false>), grid, dim3(256), shmem, s, a))
     switch (K * 2 + (dit ? 1 : 0)) {
       case 11: ZKP_NTT8(true, 5); break;
       case 13: ZKP_NTT8(true, 6); break;
