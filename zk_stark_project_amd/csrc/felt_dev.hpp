@@ -57,6 +57,51 @@ __device__ __forceinline__ uint64_t mad(uint32_t a, uint32_t b, uint64_t c) {
   asm("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=v"(d), "=s"(dead) : "v"(a), "v"(b), "v"(c));
   return d;
 }
+// the same with an inline-constant operand (-1 = 0xffffffff or 0), which
+// needs no VGPR (VOP3 takes inline constants; 0x2cff is not one)
+__device__ __forceinline__ uint32_t add_co_m1(uint32_t a, uint64_t& co) {
+  uint32_t r;
+  asm("v_add_co_u32_e64 %0, %1, %2, -1" : "=v"(r), "=s"(co) : "v"(a));
+  return r;
+}
+__device__ __forceinline__ uint32_t addc_co_0(uint32_t a, uint64_t ci, uint64_t& co) {
+  uint32_t r;
+  asm("v_addc_co_u32_e64 %0, %1, %2, 0, %3" : "=v"(r), "=s"(co) : "v"(a), "s"(ci));
+  return r;
+}
+__device__ __forceinline__ uint32_t addc_0(uint32_t a, uint64_t ci) {
+  uint32_t r;
+  uint64_t dead;
+  asm("v_addc_co_u32_e64 %0, %1, %2, 0, %3" : "=v"(r), "=s"(dead) : "v"(a), "s"(ci));
+  return r;
+}
+__device__ __forceinline__ uint32_t carry_0(uint64_t ci) {  // 0 + 0 + carry
+  uint32_t r;
+  uint64_t dead;
+  asm("v_addc_co_u32_e64 %0, %1, 0, 0, %2" : "=v"(r), "=s"(dead) : "s"(ci));
+  return r;
+}
+__device__ __forceinline__ uint32_t subb_co_0(uint32_t a, uint64_t bi, uint64_t& bo) {
+  uint32_t r;
+  asm("v_subb_co_u32_e64 %0, %1, %2, 0, %3" : "=v"(r), "=s"(bo) : "v"(a), "s"(bi));
+  return r;
+}
+__device__ __forceinline__ uint32_t subb_0(uint32_t a, uint64_t bi) {
+  uint32_t r;
+  uint64_t dead;
+  asm("v_subb_co_u32_e64 %0, %1, %2, 0, %3" : "=v"(r), "=s"(dead) : "v"(a), "s"(bi));
+  return r;
+}
+__device__ __forceinline__ uint32_t sel_0_m1(uint64_t m) {  // m ? 0xffffffff : 0
+  uint32_t r;
+  asm("v_cndmask_b32_e64 %0, 0, -1, %1" : "=v"(r) : "s"(m));
+  return r;
+}
+__device__ __forceinline__ uint64_t mul_wide(uint32_t a, uint32_t b) {  // a*b + 0 (inline)
+  uint64_t d, dead;
+  asm("v_mad_u64_u32 %0, %1, %2, %3, 0" : "=v"(d), "=s"(dead) : "v"(a), "v"(b));
+  return d;
+}
 __device__ __forceinline__ uint64_t or_mask(uint64_t a, uint64_t b) {
   uint64_t r;
   asm("s_or_b64 %0, %1, %2" : "=s"(r) : "s"(a), "s"(b) : "scc");
@@ -88,10 +133,10 @@ constexpr uint32_t P1 = 0xffffd300u;  // p = 0xffffffff_ffffffff_ffffd300_000000
 // s + C (= s - p mod 2^128) with its carry-out; result = (k | carry) ? s - p : s
 __device__ __forceinline__ felt canon_from(uint32_t s0, uint32_t s1, uint32_t s2, uint32_t s3, uint64_t k) {
   uint64_t c;
-  uint32_t t0 = add_co(s0, C0, c);
+  uint32_t t0 = add_co_m1(s0, c);
   uint32_t t1 = addc_co(s1, C1, c, c);
-  uint32_t t2 = addc_co(s2, 0u, c, c);
-  uint32_t t3 = addc_co(s3, 0u, c, c);
+  uint32_t t2 = addc_co_0(s2, c, c);
+  uint32_t t3 = addc_co_0(s3, c, c);
   uint64_t m = or_mask(k, c);
   return join(sel(s0, t0, m), sel(s1, t1, m), sel(s2, t2, m), sel(s3, t3, m));
 }
@@ -114,12 +159,12 @@ __device__ __forceinline__ felt sub(felt a, felt b) {
   uint32_t d2 = subb_co(x.w2, y.w2, bw, bw);
   uint32_t d3 = subb_co(x.w3, y.w3, bw, bw);
   // on borrow: d - C (mod 2^128) == d + p
-  uint32_t m0 = sel(0u, C0, bw), m1 = sel(0u, C1, bw);
+  uint32_t m0 = sel_0_m1(bw), m1 = sel(0u, C1, bw);
   uint64_t b2;
   uint32_t e0 = sub_co(d0, m0, b2);
   uint32_t e1 = subb_co(d1, m1, b2, b2);
-  uint32_t e2 = subb_co(d2, 0u, b2, b2);
-  uint32_t e3 = subb(d3, 0u, b2);
+  uint32_t e2 = subb_co_0(d2, b2, b2);
+  uint32_t e3 = subb_0(d3, b2);
   return join(e0, e1, e2, e3);
 }
 
@@ -128,36 +173,36 @@ __device__ __forceinline__ void mul256(L4 x, L4 y, uint32_t r[8]) {
   uint64_t acc, c;
   uint32_t ov;
   // column 0
-  acc = mad(x.w0, y.w0, 0ull);
+  acc = mul_wide(x.w0, y.w0);
   r[0] = (uint32_t)acc;
   acc >>= 32;
   // column 1
-  acc = mad_co(x.w0, y.w1, acc, c); ov = addc(0u, 0u, c);
-  acc = mad_co(x.w1, y.w0, acc, c); ov = addc(ov, 0u, c);
+  acc = mad_co(x.w0, y.w1, acc, c); ov = carry_0(c);
+  acc = mad_co(x.w1, y.w0, acc, c); ov = addc_0(ov, c);
   r[1] = (uint32_t)acc;
   acc = (acc >> 32) | ((uint64_t)ov << 32);
   // column 2
-  acc = mad_co(x.w0, y.w2, acc, c); ov = addc(0u, 0u, c);
-  acc = mad_co(x.w1, y.w1, acc, c); ov = addc(ov, 0u, c);
-  acc = mad_co(x.w2, y.w0, acc, c); ov = addc(ov, 0u, c);
+  acc = mad_co(x.w0, y.w2, acc, c); ov = carry_0(c);
+  acc = mad_co(x.w1, y.w1, acc, c); ov = addc_0(ov, c);
+  acc = mad_co(x.w2, y.w0, acc, c); ov = addc_0(ov, c);
   r[2] = (uint32_t)acc;
   acc = (acc >> 32) | ((uint64_t)ov << 32);
   // column 3
-  acc = mad_co(x.w0, y.w3, acc, c); ov = addc(0u, 0u, c);
-  acc = mad_co(x.w1, y.w2, acc, c); ov = addc(ov, 0u, c);
-  acc = mad_co(x.w2, y.w1, acc, c); ov = addc(ov, 0u, c);
-  acc = mad_co(x.w3, y.w0, acc, c); ov = addc(ov, 0u, c);
+  acc = mad_co(x.w0, y.w3, acc, c); ov = carry_0(c);
+  acc = mad_co(x.w1, y.w2, acc, c); ov = addc_0(ov, c);
+  acc = mad_co(x.w2, y.w1, acc, c); ov = addc_0(ov, c);
+  acc = mad_co(x.w3, y.w0, acc, c); ov = addc_0(ov, c);
   r[3] = (uint32_t)acc;
   acc = (acc >> 32) | ((uint64_t)ov << 32);
   // column 4
-  acc = mad_co(x.w1, y.w3, acc, c); ov = addc(0u, 0u, c);
-  acc = mad_co(x.w2, y.w2, acc, c); ov = addc(ov, 0u, c);
-  acc = mad_co(x.w3, y.w1, acc, c); ov = addc(ov, 0u, c);
+  acc = mad_co(x.w1, y.w3, acc, c); ov = carry_0(c);
+  acc = mad_co(x.w2, y.w2, acc, c); ov = addc_0(ov, c);
+  acc = mad_co(x.w3, y.w1, acc, c); ov = addc_0(ov, c);
   r[4] = (uint32_t)acc;
   acc = (acc >> 32) | ((uint64_t)ov << 32);
   // column 5
-  acc = mad_co(x.w2, y.w3, acc, c); ov = addc(0u, 0u, c);
-  acc = mad_co(x.w3, y.w2, acc, c); ov = addc(ov, 0u, c);
+  acc = mad_co(x.w2, y.w3, acc, c); ov = carry_0(c);
+  acc = mad_co(x.w3, y.w2, acc, c); ov = addc_0(ov, c);
   r[5] = (uint32_t)acc;
   acc = (acc >> 32) | ((uint64_t)ov << 32);
   // column 6 (cannot overflow: the full product is < 2^256)
@@ -170,7 +215,7 @@ __device__ __forceinline__ void mul256(L4 x, L4 y, uint32_t r[8]) {
 __device__ __forceinline__ felt reduce(const uint32_t r[8]) {
   const uint32_t K = 0x2d00u;  // 45 * 2^8
   // q = H * K (5 limbs)
-  uint64_t t = mad(r[4], K, 0ull);
+  uint64_t t = mul_wide(r[4], K);
   uint32_t q0 = (uint32_t)t;
   t = mad(r[5], K, t >> 32);
   uint32_t q1 = (uint32_t)t;
@@ -183,27 +228,27 @@ __device__ __forceinline__ felt reduce(const uint32_t r[8]) {
   uint32_t s1 = add_co(r[1], q0, c);
   uint32_t s2 = addc_co(r[2], q1, c, c);
   uint32_t s3 = addc_co(r[3], q2, c, c);
-  uint32_t s4 = addc_co(q3, 0u, c, c);
-  uint32_t s5 = addc(q4, 0u, c);
+  uint32_t s4 = addc_co_0(q3, c, c);
+  uint32_t s5 = addc_0(q4, c);
   uint64_t b;
   uint32_t x0 = sub_co(r[0], r[4], b);
   uint32_t x1 = subb_co(s1, r[5], b, b);
   uint32_t x2 = subb_co(s2, r[6], b, b);
   uint32_t x3 = subb_co(s3, r[7], b, b);
-  uint32_t x4 = subb_co(s4, 0u, b, b);
-  uint32_t x5 = subb(s5, 0u, b);
+  uint32_t x4 = subb_co_0(s4, b, b);
+  uint32_t x5 = subb_0(s5, b);
   // Y = Xl + (Xh*K)*2^32 - Xh, Xh = x4 + x5*2^32 < 2^47
-  uint64_t u = mad(x4, K, 0ull);
+  uint64_t u = mul_wide(x4, K);
   uint32_t u0 = (uint32_t)u;
   uint32_t u1 = (uint32_t)(u >> 32) + x5 * K;  // < 2^29
   uint32_t y1 = add_co(x1, u0, c);
   uint32_t y2 = addc_co(x2, u1, c, c);
-  uint32_t y3 = addc_co(x3, 0u, c, c);
+  uint32_t y3 = addc_co_0(x3, c, c);
   uint64_t top = c;  // carry past 2^128
   uint32_t z0 = sub_co(x0, x4, b);
   uint32_t z1 = subb_co(y1, x5, b, b);
-  uint32_t z2 = subb_co(y2, 0u, b, b);
-  uint32_t z3 = subb_co(y3, 0u, b, b);
+  uint32_t z2 = subb_co_0(y2, b, b);
+  uint32_t z3 = subb_co_0(y3, b, b);
   // net bit 128 = top - borrow (>= 0 overall); set when top & !borrow
   uint64_t k;
   asm("s_andn2_b64 %0, %1, %2" : "=s"(k) : "s"(top), "s"(b) : "scc");
@@ -224,20 +269,20 @@ __device__ __forceinline__ felt mul(felt a, felt b) {
 __device__ __forceinline__ void mul256x2(L4 x, L4 y, L4 u, L4 v, uint32_t r[8], uint32_t s[8]) {
   uint64_t acc, c, bcc, d;
   uint32_t ov, bov;
-  acc = mad(x.w0, y.w0, 0ull);
-  bcc = mad(u.w0, v.w0, 0ull);
+  acc = mul_wide(x.w0, y.w0);
+  bcc = mul_wide(u.w0, v.w0);
   r[0] = (uint32_t)acc; acc >>= 32;
   s[0] = (uint32_t)bcc; bcc >>= 32;
 #define ZKP_COL_BEGIN(i0, j0)                      \
   acc = mad_co(x.w##i0, y.w##j0, acc, c);          \
   bcc = mad_co(u.w##i0, v.w##j0, bcc, d);          \
-  ov = addc(0u, 0u, c);                            \
-  bov = addc(0u, 0u, d);
+  ov = carry_0(c);                                 \
+  bov = carry_0(d);
 #define ZKP_COL_STEP(i0, j0)                       \
   acc = mad_co(x.w##i0, y.w##j0, acc, c);          \
   bcc = mad_co(u.w##i0, v.w##j0, bcc, d);          \
-  ov = addc(ov, 0u, c);                            \
-  bov = addc(bov, 0u, d);
+  ov = addc_0(ov, c);                              \
+  bov = addc_0(bov, d);
 #define ZKP_COL_END(k)                             \
   r[k] = (uint32_t)acc;                            \
   s[k] = (uint32_t)bcc;                            \
@@ -260,7 +305,7 @@ __device__ __forceinline__ void mul256x2(L4 x, L4 y, L4 u, L4 v, uint32_t r[8], 
 // Two independent reductions, interleaved like mul256x2.
 __device__ __forceinline__ void reduce_x2(const uint32_t r[8], const uint32_t s[8], felt& out_r, felt& out_s) {
   const uint32_t K = 0x2d00u;
-  uint64_t t = mad(r[4], K, 0ull), tt = mad(s[4], K, 0ull);
+  uint64_t t = mul_wide(r[4], K), tt = mul_wide(s[4], K);
   uint32_t q0 = (uint32_t)t, p0 = (uint32_t)tt;
   t = mad(r[5], K, t >> 32); tt = mad(s[5], K, tt >> 32);
   uint32_t q1 = (uint32_t)t, p1 = (uint32_t)tt;
@@ -281,17 +326,17 @@ __device__ __forceinline__ void reduce_x2(const uint32_t r[8], const uint32_t s[
   uint32_t S3 = addc_co(s[3], p2, e, e);
   uint32_t x2 = subb_co(s2, r[6], b, b);
   uint32_t X2 = subb_co(S2, s[6], f, f);
-  uint32_t s4 = addc_co(q3, 0u, c, c);
-  uint32_t S4 = addc_co(p3, 0u, e, e);
+  uint32_t s4 = addc_co_0(q3, c, c);
+  uint32_t S4 = addc_co_0(p3, e, e);
   uint32_t x3 = subb_co(s3, r[7], b, b);
   uint32_t X3 = subb_co(S3, s[7], f, f);
-  uint32_t s5 = addc(q4, 0u, c);
-  uint32_t S5 = addc(p4, 0u, e);
-  uint32_t x4 = subb_co(s4, 0u, b, b);
-  uint32_t X4 = subb_co(S4, 0u, f, f);
-  uint32_t x5 = subb(s5, 0u, b);
-  uint32_t X5 = subb(S5, 0u, f);
-  uint64_t uu = mad(x4, K, 0ull), UU = mad(X4, K, 0ull);
+  uint32_t s5 = addc_0(q4, c);
+  uint32_t S5 = addc_0(p4, e);
+  uint32_t x4 = subb_co_0(s4, b, b);
+  uint32_t X4 = subb_co_0(S4, f, f);
+  uint32_t x5 = subb_0(s5, b);
+  uint32_t X5 = subb_0(S5, f);
+  uint64_t uu = mul_wide(x4, K), UU = mul_wide(X4, K);
   uint32_t u0 = (uint32_t)uu, U0 = (uint32_t)UU;
   uint32_t u1 = (uint32_t)(uu >> 32) + x5 * K, U1 = (uint32_t)(UU >> 32) + X5 * K;
   uint32_t y1 = add_co(x1, u0, c);
@@ -302,25 +347,25 @@ __device__ __forceinline__ void reduce_x2(const uint32_t r[8], const uint32_t s[
   uint32_t Y2 = addc_co(X2, U1, e, e);
   uint32_t z1 = subb_co(y1, x5, b, b);
   uint32_t Z1 = subb_co(Y1, X5, f, f);
-  uint32_t y3 = addc_co(x3, 0u, c, c);
-  uint32_t Y3 = addc_co(X3, 0u, e, e);
-  uint32_t z2 = subb_co(y2, 0u, b, b);
-  uint32_t Z2 = subb_co(Y2, 0u, f, f);
-  uint32_t z3 = subb_co(y3, 0u, b, b);
-  uint32_t Z3 = subb_co(Y3, 0u, f, f);
+  uint32_t y3 = addc_co_0(x3, c, c);
+  uint32_t Y3 = addc_co_0(X3, e, e);
+  uint32_t z2 = subb_co_0(y2, b, b);
+  uint32_t Z2 = subb_co_0(Y2, f, f);
+  uint32_t z3 = subb_co_0(y3, b, b);
+  uint32_t Z3 = subb_co_0(Y3, f, f);
   uint64_t k1, k2;
   asm("s_andn2_b64 %0, %1, %2" : "=s"(k1) : "s"(c), "s"(b) : "scc");
   asm("s_andn2_b64 %0, %1, %2" : "=s"(k2) : "s"(e), "s"(f) : "scc");
   // canonicalize both (interleaved)
   uint64_t g1, g2;
-  uint32_t t0 = add_co(z0, C0, g1);
-  uint32_t T0 = add_co(Z0, C0, g2);
+  uint32_t t0 = add_co_m1(z0, g1);
+  uint32_t T0 = add_co_m1(Z0, g2);
   uint32_t t1 = addc_co(z1, C1, g1, g1);
   uint32_t T1 = addc_co(Z1, C1, g2, g2);
-  uint32_t t2 = addc_co(z2, 0u, g1, g1);
-  uint32_t T2 = addc_co(Z2, 0u, g2, g2);
-  uint32_t t3 = addc_co(z3, 0u, g1, g1);
-  uint32_t T3 = addc_co(Z3, 0u, g2, g2);
+  uint32_t t2 = addc_co_0(z2, g1, g1);
+  uint32_t T2 = addc_co_0(Z2, g2, g2);
+  uint32_t t3 = addc_co_0(z3, g1, g1);
+  uint32_t T3 = addc_co_0(Z3, g2, g2);
   uint64_t m1 = or_mask(k1, g1), m2 = or_mask(k2, g2);
   out_r = join(sel(z0, t0, m1), sel(z1, t1, m1), sel(z2, t2, m1), sel(z3, t3, m1));
   out_s = join(sel(Z0, T0, m2), sel(Z1, T1, m2), sel(Z2, T2, m2), sel(Z3, T3, m2));
@@ -345,15 +390,15 @@ __device__ __forceinline__ void addsub(felt a, felt b, felt& sum, felt& diff) {
   uint32_t s3 = addc_co(x.w3, y.w3, c, c);
   uint32_t d3 = subb_co(x.w3, y.w3, bw, bw);
   uint64_t g, b2;
-  uint32_t m0 = sel(0u, C0, bw), m1 = sel(0u, C1, bw);
-  uint32_t t0 = add_co(s0, C0, g);
+  uint32_t m0 = sel_0_m1(bw), m1 = sel(0u, C1, bw);
+  uint32_t t0 = add_co_m1(s0, g);
   uint32_t e0 = sub_co(d0, m0, b2);
   uint32_t t1 = addc_co(s1, C1, g, g);
   uint32_t e1 = subb_co(d1, m1, b2, b2);
-  uint32_t t2 = addc_co(s2, 0u, g, g);
-  uint32_t e2 = subb_co(d2, 0u, b2, b2);
-  uint32_t t3 = addc_co(s3, 0u, g, g);
-  uint32_t e3 = subb(d3, 0u, b2);
+  uint32_t t2 = addc_co_0(s2, g, g);
+  uint32_t e2 = subb_co_0(d2, b2, b2);
+  uint32_t t3 = addc_co_0(s3, g, g);
+  uint32_t e3 = subb_0(d3, b2);
   uint64_t m = or_mask(c, g);
   sum = join(sel(s0, t0, m), sel(s1, t1, m), sel(s2, t2, m), sel(s3, t3, m));
   diff = join(e0, e1, e2, e3);
