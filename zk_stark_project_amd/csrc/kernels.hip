@@ -1052,12 +1052,36 @@ __device__ __forceinline__ void block_batch_inverse(felt* v, felt* s_pre, felt* 
 // (x_q - c0)(x_q - c1) (or (x_q - c0) when !two) of each block's EVAL_CH*TPB
 // local points q (EVAL_POINT), x_q = point_x(m, q). Same point->block mapping
 // as the phase-3 kernels.
+// With pw (DEEP: pw[l] = c0^(2^l), pw[logn + l] = c1^(2^l)), block 0 also writes
+// the inverse of the product over ALL points to *tinv, from the closed form
+// prod_t (cx_j w_n^t - c) = c^n - cx_j^n per coset (n even): prod_j (c0^n -
+// cx_j^n)(c1^n - cx_j^n). Its field inversion then runs beside the other
+// blocks instead of after them in k_invert_products.
 __global__ __launch_bounds__(TPB) void k_den_products(PointMap m, uint64_t count, felt c0, felt c1, int two,
-                                                      const felt* __restrict__ cdev, felt* __restrict__ prod) {
+                                                      const felt* __restrict__ cdev, const felt* __restrict__ pw,
+                                                      felt* __restrict__ tinv, felt* __restrict__ prod) {
   __shared__ felt s[TPB];
   if (cdev) {  // points drawn on the device (DEEP: z, z*w_n)
     c0 = cdev[0];
     c1 = cdev[1];
+  }
+  if (pw && blockIdx.x == 0) {
+    const uint32_t ncos = (uint32_t)(count >> m.logn);
+    const felt zn = sqr(pw[m.logn - 1]), zgn = sqr(pw[2 * m.logn - 1]);
+    felt acc = one();
+    for (uint32_t j = threadIdx.x; j < ncos; j += TPB) {
+      felt cn = m.cx[j];
+      for (uint32_t l = 0; l < m.logn; l++) cn = sqr(cn);
+      acc = mul(acc, mul(sub(zn, cn), sub(zgn, cn)));
+    }
+    s[threadIdx.x] = acc;
+    __syncthreads();
+    for (uint32_t h = TPB / 2; h >= 1; h >>= 1) {
+      if (threadIdx.x < h) s[threadIdx.x] = mul(s[threadIdx.x], s[threadIdx.x + h]);
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) *tinv = inv(s[0]);
+    __syncthreads();
   }
   felt acc = one();
   static_for<0, EVAL_CH>([&](auto k) {
@@ -1078,8 +1102,9 @@ __global__ __launch_bounds__(TPB) void k_den_products(PointMap m, uint64_t count
   if (threadIdx.x == 0) prod[blockIdx.x] = s[0];
 }
 
-// Phase 2: invert all block products in place with one field inversion.
-__global__ __launch_bounds__(1024) void k_invert_products(felt* prod, uint32_t nb) {
+// Phase 2: invert all block products in place with one field inversion (or
+// none: tinv = the inverse of their product, precomputed by k_den_products).
+__global__ __launch_bounds__(1024) void k_invert_products(felt* prod, uint32_t nb, const felt* __restrict__ tinv) {
   __shared__ felt s_pre[1024], s_suf[1024];
   __shared__ felt s_inv;
   const uint32_t t = threadIdx.x;
@@ -1100,7 +1125,7 @@ __global__ __launch_bounds__(1024) void k_invert_products(felt* prod, uint32_t n
     s_suf[t] = mul(s_suf[t], b);
     __syncthreads();
   }
-  if (t == 0) s_inv = inv(s_pre[1023]);
+  if (t == 0) s_inv = tinv ? *tinv : inv(s_pre[1023]);
   __syncthreads();
   felt ia = s_inv;
   if (t > 0) ia = mul(ia, s_pre[t - 1]);
@@ -1246,12 +1271,15 @@ __global__ __launch_bounds__(TPB) void k_eval_linear(EvalCommon c, LinearEvalArg
 
 // bit-reversed polynomial evaluation: tree with level multipliers x^(2^l)
 constexpr uint32_t OOD_LOGE = 11;
+// Arrays a >= ntwo (the composition columns, whose OOD frame is at z only) skip
+// the second point (their partials at it are left zero).
 __global__ __launch_bounds__(TPB) void k_eval_bitrev(const felt* __restrict__ arrays, uint32_t logn, uint32_t logE,
                                                      const felt* __restrict__ pw0, const felt* __restrict__ pw1,
-                                                     felt* __restrict__ partial) {
+                                                     uint32_t ntwo, felt* __restrict__ partial) {
   __shared__ felt s0[TPB];
   __shared__ felt s1[TPB];
   const uint32_t E = 1u << logE;
+  const bool two = blockIdx.y < ntwo;  // block-uniform
   const felt* src = arrays + ((uint64_t)blockIdx.y << logn) + ((uint64_t)blockIdx.x << logE);
   const uint32_t t = threadIdx.x;
   // levels 0..2 in registers over the thread's 8 consecutive elements (E = 2048 = 8 * TPB),
@@ -1265,17 +1293,20 @@ __global__ __launch_bounds__(TPB) void k_eval_bitrev(const felt* __restrict__ ar
     {
       const felt m0 = pw0[logn - 1], m1 = pw1[logn - 1];
 #pragma unroll
-      for (int i = 0; i < 4; i++) { a[i] = add(v[2 * i], mul(m0, v[2 * i + 1])); b[i] = add(v[2 * i], mul(m1, v[2 * i + 1])); }
+      for (int i = 0; i < 4; i++) a[i] = add(v[2 * i], mul(m0, v[2 * i + 1]));
+      if (two)
+#pragma unroll
+        for (int i = 0; i < 4; i++) b[i] = add(v[2 * i], mul(m1, v[2 * i + 1]));
     }
     {
       const felt m0 = pw0[logn - 2], m1 = pw1[logn - 2];
       a[0] = add(a[0], mul(m0, a[1])); a[2] = add(a[2], mul(m0, a[3]));
-      b[0] = add(b[0], mul(m1, b[1])); b[2] = add(b[2], mul(m1, b[3]));
+      if (two) { b[0] = add(b[0], mul(m1, b[1])); b[2] = add(b[2], mul(m1, b[3])); }
     }
     {
       const felt m0 = pw0[logn - 3], m1 = pw1[logn - 3];
       s0[t] = add(a[0], mul(m0, a[2]));
-      s1[t] = add(b[0], mul(m1, b[2]));
+      s1[t] = two ? add(b[0], mul(m1, b[2])) : zero();
     }
     l = 3;
     m = TPB;
@@ -1304,7 +1335,7 @@ __global__ __launch_bounds__(TPB) void k_eval_bitrev(const felt* __restrict__ ar
     if (t < m / (2 * d)) {
       uint32_t p = t * 2 * d;
       s0[p] = add(s0[p], mul(m0, s0[p + d]));
-      s1[p] = add(s1[p], mul(m1, s1[p + d]));
+      if (two) s1[p] = add(s1[p], mul(m1, s1[p + d]));
     }
     __syncthreads();
   }
@@ -1937,13 +1968,15 @@ void launch_grind(Prof& prof, hipStream_t s, const uint32_t* seed_words, uint64_
          hipLaunchKernelGGL(k_grind, dim3(blocks_for(count)), dim3(TPB), 0, s, sa, base, count, bits, result));
 }
 
+// prod: nb block products (+1 slot for the closed-form total inverse when pw is given)
 static void launch_den_inverse(Prof& prof, hipStream_t s, const PointMap& m, uint64_t count, felt c0, felt c1,
-                               int two, felt* prod, const felt* cdev = nullptr) {
+                               int two, felt* prod, const felt* cdev = nullptr, const felt* pw = nullptr) {
   uint32_t nb = blocks_for((count + EVAL_CH - 1) / EVAL_CH);
+  felt* tinv = pw ? prod + nb : nullptr;
   LAUNCH(prof, "den_products", s, (double)count * 16.0,
-         hipLaunchKernelGGL(k_den_products, dim3(nb), dim3(TPB), 0, s, m, count, c0, c1, two, cdev, prod));
+         hipLaunchKernelGGL(k_den_products, dim3(nb), dim3(TPB), 0, s, m, count, c0, c1, two, cdev, pw, tinv, prod));
   LAUNCH(prof, "invert_products", s, (double)nb * 32.0,
-         hipLaunchKernelGGL(k_invert_products, dim3(1), dim3(1024), 0, s, prod, nb));
+         hipLaunchKernelGGL(k_invert_products, dim3(1), dim3(1024), 0, s, prod, nb, tinv));
 }
 
 static void launch_den_table(Prof& prof, hipStream_t s, const PointMap& m, uint64_t count, felt c0, felt c1,
@@ -1981,21 +2014,22 @@ void launch_eval_linear(Prof& prof, hipStream_t s, const EvalCommon& c, const Li
            hipLaunchKernelGGL((k_eval_linear<true, true>), g, dim3(TPB), 0, s, c, a, lde, a.dinv, comp));
 }
 
-void launch_eval_bitrev(Prof& prof, hipStream_t s, const felt* arrays, uint32_t narrays, uint32_t logn,
+void launch_eval_bitrev(Prof& prof, hipStream_t s, const felt* arrays, uint32_t narrays, uint32_t ntwo, uint32_t logn,
                         const felt* pw0, const felt* pw1, felt* partial, felt ninv, felt* out) {
   uint32_t logE = logn < OOD_LOGE ? logn : OOD_LOGE;
   uint32_t nb = 1u << (logn - logE);
   LAUNCH(prof, "eval_bitrev", s, (double)narrays * (1ull << logn) * 16.0,
          hipLaunchKernelGGL(k_eval_bitrev, dim3(nb, narrays), dim3(TPB), 0, s, arrays, logn, logE, pw0, pw1,
-                            partial));
+                            ntwo, partial));
   LAUNCH(prof, "eval_bitrev_tail", s, (double)narrays * nb * 32.0,
          hipLaunchKernelGGL(k_eval_bitrev_tail, dim3(narrays), dim3(TPB), 0, s, partial, nb, logn, logE, pw0, pw1,
                             ninv, out));
 }
 
 void launch_deep_denominators(Prof& prof, hipStream_t s, const PointMap& m, uint64_t count, const felt* zz,
-                              felt* binv) {
-  launch_den_inverse(prof, s, m, count, zero(), zero(), 1, binv, zz);
+                              const felt* pw, felt* binv) {
+  if (count & ((1ull << m.logn) - 1)) abort();  // whole cosets only (closed-form total)
+  launch_den_inverse(prof, s, m, count, zero(), zero(), 1, binv, zz, pw);
 }
 
 void launch_deep(Prof& prof, hipStream_t s, const DeepArgs& a, felt* out) {

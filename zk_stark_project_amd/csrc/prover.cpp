@@ -373,13 +373,15 @@ void fetch_all(zkp_ctx* ctx, const std::vector<Fetch>& fs) {
 
 // OOD values of bit-reversed arrays at the two points whose power tables
 // dpw[0..logn) / dpw[logn..2logn) are in device memory; returns the device
-// array ood[2a + {0,1}] (array a at the two points)
-felt* ood_launch(zkp_ctx* ctx, const felt* arrays, uint32_t narrays, uint32_t logn, const felt* dpw) {
+// array ood[2a + {0,1}] (array a at the two points; arrays a >= ntwo at the
+// first point only, their second entry is zero)
+felt* ood_launch(zkp_ctx* ctx, const felt* arrays, uint32_t narrays, uint32_t ntwo, uint32_t logn,
+                 const felt* dpw) {
   uint32_t logE = logn < 11 ? logn : 11;
   if (logn - logE > 12) throw ZkpFail{ZKP_ERR_TRACE_SHAPE, "OOD evaluation supports n <= 2^23"};
   felt* part = ctx->buf<felt>("ood_part", (size_t)2 * narrays * (1ull << (logn - logE)));
   felt* dv = ctx->buf<felt>("ood_vals", (size_t)2 * narrays);
-  launch_eval_bitrev(ctx->prof, ctx->stream, arrays, narrays, logn, dpw, dpw + logn, part,
+  launch_eval_bitrev(ctx->prof, ctx->stream, arrays, narrays, ntwo, logn, dpw, dpw + logn, part,
                      inv(felt_u64(1ull << logn)), dv);
   return dv;
 }
@@ -633,16 +635,16 @@ int prove_impl(zkp_ctx* ctx, zkp_comm* cm, int air_id, const felt* d_trace, uint
 
   // 5. OOD frame (every rank holds all trace and composition coefficients)
   // the DEEP denominators (x - z)(x - zg) only need z: their batch-inversion
-  // phases run on the side stream while the host finishes the OOD transcript
+  // phases run on the side stream beside the OOD evaluation and its transcript
   felt* deep_binv = ctx->buf<felt>("binv", ((uint64_t)Bl * n) / 2048 + 1);
   const PointMap deep_pm{cx + j0, twn, logn};
   HIP_CHECK(hipEventRecord(ctx->ev_fork, st));
   HIP_CHECK(hipStreamWaitEvent(ctx->side, ctx->ev_fork, 0));
-  launch_deep_denominators(pf, ctx->side, deep_pm, (uint64_t)Bl * n, dt_zz, deep_binv);
+  launch_deep_denominators(pf, ctx->side, deep_pm, (uint64_t)Bl * n, dt_zz, dt_pw, deep_binv);
   HIP_CHECK(hipEventRecord(ctx->ev_join, ctx->side));
   // OOD frame and DEEP coefficients on the device (device transcript); the host
   // replays both at the FRI round trip
-  felt* dv = ood_launch(ctx, coef, w + C, logn, dt_pw);
+  felt* dv = ood_launch(ctx, coef, w + C, w, logn, dt_pw);  // composition columns at z only
   felt* dgam = ctx->buf<felt>("gamma", w + C);
   felt* dk = ctx->buf<felt>("dt_dk", 4);
   HIP_CHECK(hipMemcpyAsync(dk, dt_zz, 32, hipMemcpyDeviceToDevice, st));

@@ -163,7 +163,8 @@ void launch_comp_dft(Prof& prof, hipStream_t s, const felt* recv, const uint32_t
 
 // OOD evaluation of bit-reversed arrays (arrays contiguous, stride n) at x0 and x1
 // partial[(a * nblocks + b) * 2 + {0,1}] ; pw0/pw1 = x^(2^l) tables (logn entries, device)
-void launch_eval_bitrev(Prof& prof, hipStream_t s, const felt* arrays, uint32_t narrays, uint32_t logn,
+// (arrays a >= ntwo at x0 only)
+void launch_eval_bitrev(Prof& prof, hipStream_t s, const felt* arrays, uint32_t narrays, uint32_t ntwo, uint32_t logn,
                         const felt* pw0, const felt* pw1, felt* partial, felt ninv, felt* out);
 
 // DEEP composition over the LDE domain (natural order out)
@@ -181,7 +182,7 @@ struct DeepArgs {
 // phases 1-2 of the DEEP batch inversion (block inverse products of (x - z)(x - zg)
 // into binv); launch_deep then runs phase 3 + the composition
 void launch_deep_denominators(Prof& prof, hipStream_t s, const PointMap& m, uint64_t count, const felt* zz,
-                              felt* binv);
+                              const felt* pw, felt* binv);
 void launch_deep(Prof& prof, hipStream_t s, const DeepArgs& a, felt* out);
 
 // FRI fold-by-F (F = 16) over coset-major evaluations of the cosets [j0, j0+Bl)
