@@ -988,14 +988,58 @@ struct SeedArg {
   uint32_t w[8];
 };
 
-__global__ __launch_bounds__(TPB) void k_grind(SeedArg seed, uint64_t base, uint64_t count, uint32_t bits,
-                                               unsigned long long* result) {
+// FriProver::set_remainder on the device for small last layers (D <= 256): the
+// D values E (coset-major: natural index i = j + B*t at E[j*m + t]) interpolated
+// over off*<w_D>, the first ncoef = D/B coefficients kept:
+// c_k = D^-1 off^-k sum_i v_i w_D^-ik. Then the coin absorbs H(remainder)
+// (seed <- BLAKE3(seed || H)) so grinding can start from the device seed.
+// rem_out = [ncoef coefficients], commit_out = H(remainder) (8 words).
+__global__ __launch_bounds__(TPB) void k_fri_remainder(const felt* __restrict__ E, uint32_t logB, uint32_t m,
+                                                       felt off_inv, felt wd_inv, felt d_inv, uint32_t ncoef,
+                                                       uint32_t* __restrict__ seed, felt* __restrict__ rem_out,
+                                                       uint32_t* __restrict__ commit_out) {
+  __shared__ felt s_c[256];
+  __shared__ uint32_t s_cv[32][8];
+  const uint32_t D = m << logB;
+  for (uint32_t k = threadIdx.x; k < ncoef; k += TPB) {
+    const felt wk = fp::pow_u64(wd_inv, k);
+    felt p = one(), acc = zero();
+    for (uint32_t i = 0; i < D; i++) {
+      acc = add(acc, mul(E[(i & ((1u << logB) - 1)) * m + (i >> logB)], p));
+      p = mul(p, wk);
+    }
+    const felt c = mul(mul(acc, d_inv), fp::pow_u64(off_inv, k));
+    s_c[k] = c;
+    rem_out[k] = c;
+  }
+  __syncthreads();
+  uint32_t h[8];
+  hash_felts_block([&](uint32_t i) { return s_c[i]; }, ncoef, h, s_cv);
+  if (threadIdx.x == 0) {
+    uint32_t t[8];
+    for (int i = 0; i < 8; i++) t[i] = seed[i];
+    dcoin_reseed(t, h);
+    for (int i = 0; i < 8; i++) { seed[i] = t[i]; commit_out[i] = h[i]; }
+  }
+}
+
+// Minimum nonce in [base, base + count) whose BLAKE3(seed || nonce) has >= bits
+// trailing zeros (atomicMin). seedp (device coin state) overrides seed. A block
+// whose nonces all exceed a result already found exits at once (blocks are
+// dispatched in index order, so most blocks after the first hit do no work).
+__global__ __launch_bounds__(TPB) void k_grind(SeedArg seed, const uint32_t* __restrict__ seedp, uint64_t base,
+                                               uint64_t count, uint32_t bits, unsigned long long* result) {
+  __shared__ int s_skip;
+  const uint64_t b0 = base + blockIdx.x * (uint64_t)TPB;
+  if (threadIdx.x == 0) s_skip = __hip_atomic_load(result, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < b0;
+  __syncthreads();
+  if (s_skip) return;
   uint64_t i = blockIdx.x * (uint64_t)TPB + threadIdx.x;
   if (i >= count) return;
   uint64_t nonce = base + i;
   uint32_t m[16];
 #pragma unroll
-  for (int k = 0; k < 8; k++) m[k] = seed.w[k];
+  for (int k = 0; k < 8; k++) m[k] = seedp ? seedp[k] : seed.w[k];
   m[8] = (uint32_t)nonce;
   m[9] = (uint32_t)(nonce >> 32);
 #pragma unroll
@@ -1960,12 +2004,22 @@ void launch_merkle_tree(Prof& prof, hipStream_t s, uint32_t* nodes, uint64_t L) 
     LAUNCH(prof, "merkle_top", s, (double)lvl * 2.0 * 96.0, hipLaunchKernelGGL(k_merkle_top, dim3(1), dim3(1024), 0, s, nodes, lvl));
 }
 
-void launch_grind(Prof& prof, hipStream_t s, const uint32_t* seed_words, uint64_t base, uint64_t count,
-                  uint32_t bits, unsigned long long* result) {
+void launch_grind(Prof& prof, hipStream_t s, const uint32_t* seed_words, const uint32_t* seed_dev, uint64_t base,
+                  uint64_t count, uint32_t bits, unsigned long long* result) {
   SeedArg sa;
-  for (int i = 0; i < 8; i++) sa.w[i] = seed_words[i];
+  for (int i = 0; i < 8; i++) sa.w[i] = seed_words ? seed_words[i] : 0u;
   LAUNCH(prof, "grind", s, 0.0,
-         hipLaunchKernelGGL(k_grind, dim3(blocks_for(count)), dim3(TPB), 0, s, sa, base, count, bits, result));
+         hipLaunchKernelGGL(k_grind, dim3(blocks_for(count)), dim3(TPB), 0, s, sa, seed_dev, base, count, bits,
+                            result));
+}
+
+void launch_fri_remainder(Prof& prof, hipStream_t s, const felt* E, uint32_t logB, uint32_t m, felt off_inv,
+                          felt wd_inv, felt d_inv, uint32_t* seed, felt* rem_out, uint32_t* commit_out) {
+  const uint32_t D = m << logB, ncoef = m;
+  if (D > 256) abort();  // the caller keeps larger remainders on the host
+  LAUNCH(prof, "coin", s, 0.0,
+         hipLaunchKernelGGL(k_fri_remainder, dim3(1), dim3(TPB), 0, s, E, logB, m, off_inv, wd_inv, d_inv, ncoef,
+                            seed, rem_out, commit_out));
 }
 
 // prod: nb block products (+1 slot for the closed-form total inverse when pw is given)

@@ -684,6 +684,12 @@ int prove_impl(zkp_ctx* ctx, zkp_comm* cm, int air_id, const felt* d_trace, uint
   };
   std::vector<Layer> layers(L + 1);
   std::vector<felt> remainder;
+  bool dev_tail = false;  // remainder + first grinding chunk on the device
+  felt* rem_d = nullptr;
+  uint32_t* rcommit_d = nullptr;
+  unsigned long long* dres = ctx->buf<unsigned long long>("grind_res", 1);
+  unsigned long long dnonce = ~0ull;
+  const uint64_t grind_chunk = 1ull << 22;
   {
     uint64_t tot_e = 0, D = N;
     for (uint32_t l = 0; l < L; l++) { tot_e += D / F; D /= F; }
@@ -741,6 +747,19 @@ int prove_impl(zkp_ctx* ctx, zkp_comm* cm, int air_id, const felt* d_trace, uint
     }
     if (sh) replicate(L);
     layers[L].E = E; layers[L].m = m; layers[L].Bc = B; layers[L].jc = 0; layers[L].sharded = false;
+    // small remainders: remainder, its commitment, the coin reseed and the first
+    // grinding chunk run on the device too, so the round trip below also
+    // returns the nonce (the host replays and checks all of it)
+    const uint64_t Dlast = (uint64_t)B * m;
+    dev_tail = Dlast <= 256 && o->grinding_factor > 0;
+    if (dev_tail) {
+      rem_d = ctx->buf<felt>("rem_d", m + 1);
+      rcommit_d = ctx->buf<uint32_t>("rem_commit", 8);
+      launch_fri_remainder(pf, st, E, logB, (uint32_t)m, inv(off), inv(root_of_unity(ilog2(Dlast))),
+                           inv(felt_u64(Dlast)), coin_d, rem_d, rcommit_d);
+      HIP_CHECK(hipMemsetAsync(dres, 0xff, 8, st));
+      launch_grind(pf, st, nullptr, coin_d, 1, grind_chunk, o->grinding_factor, dres);
+    }
     // the proof's first host round trip: the device transcript so far (commitment
     // roots, coefficients, z, OOD frame, DEEP coefficients, FRI roots + alphas)
     // and the last FRI layer
@@ -748,12 +767,20 @@ int prove_impl(zkp_ctx* ctx, zkp_comm* cm, int air_id, const felt* d_trace, uint
     std::vector<felt> dalpha(L);
     std::vector<felt> cm_vals((size_t)B * m);
     std::vector<felt> dcc(ncoef), dzz(2), hood((size_t)2 * (w + C)), hgam(w + C), hdk(4);
-    uint8_t roots[64];
-    fetch_all(ctx, {{dalpha.data(), alphas_d, (size_t)L * 16}, {rb.data(), roots_d, (size_t)L * 32},
-                    {cm_vals.data(), E, cm_vals.size() * 16}, {dcc.data(), dt_cc, (size_t)ncoef * 16},
-                    {dzz.data(), dt_zz, 32}, {hood.data(), dv, hood.size() * 16},
-                    {hgam.data(), dgam, hgam.size() * 16}, {hdk.data(), dk, 64},
-                    {roots, troot_d, 32}, {roots + 32, croot_d, 32}});
+    std::vector<felt> drem(dev_tail ? m : 0);
+    uint8_t roots[64], drcommit[32], dseed[32];
+    std::vector<Fetch> fs = {{dalpha.data(), alphas_d, (size_t)L * 16}, {rb.data(), roots_d, (size_t)L * 32},
+                             {cm_vals.data(), E, cm_vals.size() * 16}, {dcc.data(), dt_cc, (size_t)ncoef * 16},
+                             {dzz.data(), dt_zz, 32}, {hood.data(), dv, hood.size() * 16},
+                             {hgam.data(), dgam, hgam.size() * 16}, {hdk.data(), dk, 64},
+                             {roots, troot_d, 32}, {roots + 32, croot_d, 32}};
+    if (dev_tail) {
+      fs.push_back({drem.data(), rem_d, drem.size() * 16});
+      fs.push_back({drcommit, rcommit_d, 32});
+      fs.push_back({dseed, coin_d, 32});
+      fs.push_back({&dnonce, dres, 8});
+    }
+    fetch_all(ctx, fs);
     memcpy(T.trace_root, roots, 32);
     memcpy(T.constraint_root, roots + 32, 32);
     if (R == 1) {
@@ -799,6 +826,11 @@ int prove_impl(zkp_ctx* ctx, zkp_comm* cm, int air_id, const felt* d_trace, uint
     remainder.resize(D / B);
     hash_elements(remainder.data(), remainder.size(), T.remainder_commitment);
     coin.reseed(T.remainder_commitment);
+    if (dev_tail) {
+      bool ok = memcmp(drcommit, T.remainder_commitment, 32) == 0 && memcmp(dseed, coin.seed, 32) == 0;
+      for (size_t i = 0; i < drem.size() && ok; i++) ok = eq(drem[i], remainder[i]);
+      if (!ok) throw ZkpFail{ZKP_ERR_DEVICE, "device remainder / grinding seed diverged from the host"};
+    }
     T.num_fri_layers = L;
   }
   ctx->stage_end("5_fri");
@@ -808,16 +840,20 @@ int prove_impl(zkp_ctx* ctx, zkp_comm* cm, int air_id, const felt* d_trace, uint
   if (o->grinding_factor == 0) {
     nonce = 1;
   } else {
-    unsigned long long* dres = ctx->buf<unsigned long long>("grind_res", 1);
     uint32_t sw[8];
     for (int i = 0; i < 8; i++)
       sw[i] = (uint32_t)coin.seed[4 * i] | ((uint32_t)coin.seed[4 * i + 1] << 8) |
               ((uint32_t)coin.seed[4 * i + 2] << 16) | ((uint32_t)coin.seed[4 * i + 3] << 24);
-    const uint64_t chunk = 1ull << 22;
-    for (uint64_t base = 1; nonce == 0; base += chunk) {
+    const uint64_t chunk = grind_chunk;
+    uint64_t base0 = 1;
+    if (dev_tail) {  // the first chunk ran on the device seed (checked equal to coin.seed above)
+      if (dnonce != ~0ull) nonce = dnonce;
+      base0 = 1 + chunk;
+    }
+    for (uint64_t base = base0; nonce == 0; base += chunk) {
       unsigned long long init = ~0ull;
       ctx->upload(dres, &init, 8);
-      launch_grind(pf, st, sw, base, chunk, o->grinding_factor, dres);
+      launch_grind(pf, st, sw, nullptr, base, chunk, o->grinding_factor, dres);
       unsigned long long res;
       ctx->download(&res, dres, 8);
       if (res != ~0ull) nonce = res;
@@ -1281,7 +1317,7 @@ int zkp_grind(zkp_ctx* ctx, const uint8_t seed[32], uint32_t bits, uint64_t* non
     for (uint64_t base = 1;; base += chunk) {
       unsigned long long init = ~0ull, res;
       ctx->upload(dres, &init, 8);
-      launch_grind(ctx->prof, ctx->stream, sw, base, chunk, bits, dres);
+      launch_grind(ctx->prof, ctx->stream, sw, nullptr, base, chunk, bits, dres);
       ctx->download(&res, dres, 8);
       if (res != ~0ull) { *nonce = res; break; }
       if (base > (1ull << 40)) return (int)ZKP_ERR_NONCE;

@@ -83,8 +83,13 @@ void launch_merkle_from_shards(Prof& prof, hipStream_t s, const uint32_t* recv, 
                                uint32_t* nodes);
 // internal nodes nodes[1..L) from leaves nodes[L..2L)
 void launch_merkle_tree(Prof& prof, hipStream_t s, uint32_t* nodes, uint64_t L);
-void launch_grind(Prof& prof, hipStream_t s, const uint32_t* seed_words_dev, uint64_t base, uint64_t count,
-                  uint32_t bits, unsigned long long* result);
+// seed from host words, or (seed_words == nullptr) from the device coin state seed_dev
+void launch_grind(Prof& prof, hipStream_t s, const uint32_t* seed_words, const uint32_t* seed_dev, uint64_t base,
+                  uint64_t count, uint32_t bits, unsigned long long* result);
+// remainder of a last FRI layer of D = m * 2^logB <= 256 values (coefficients
+// rem_out[0..m)), commitment H(remainder) and the coin reseed with it (seed in place)
+void launch_fri_remainder(Prof& prof, hipStream_t s, const felt* E, uint32_t logB, uint32_t m, felt off_inv,
+                          felt wd_inv, felt d_inv, uint32_t* seed, felt* rem_out, uint32_t* commit_out);
 
 // ---------------------------------------------------------------- device transcript
 // (seed = 8 LE words of the DefaultRandomCoin state, in device memory)
