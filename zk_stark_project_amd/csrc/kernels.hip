@@ -988,6 +988,18 @@ struct SeedArg {
   uint32_t w[8];
 };
 
+// gathers up to PACK_MAX device segments (4-byte multiples) into one staging
+// buffer, so a host round trip is one kernel + one D2H copy instead of one
+// copy call per segment
+__global__ __launch_bounds__(TPB) void k_pack(PackArgs a, uint32_t* __restrict__ dst) {
+  const uint32_t seg = blockIdx.y;
+  if (seg >= a.n) return;
+  const uint32_t* src = reinterpret_cast<const uint32_t*>(a.src[seg]);
+  const uint64_t words = a.bytes[seg] / 4, o = a.off[seg] / 4;
+  for (uint64_t i = blockIdx.x * (uint64_t)TPB + threadIdx.x; i < words; i += (uint64_t)gridDim.x * TPB)
+    dst[o + i] = src[i];
+}
+
 // FriProver::set_remainder on the device for small last layers (D <= 256): the
 // D values E (coset-major: natural index i = j + B*t at E[j*m + t]) interpolated
 // over off*<w_D>, the first ncoef = D/B coefficients kept:
@@ -2011,6 +2023,14 @@ void launch_grind(Prof& prof, hipStream_t s, const uint32_t* seed_words, const u
   LAUNCH(prof, "grind", s, 0.0,
          hipLaunchKernelGGL(k_grind, dim3(blocks_for(count)), dim3(TPB), 0, s, sa, seed_dev, base, count, bits,
                             result));
+}
+
+void launch_pack(Prof& prof, hipStream_t s, const PackArgs& a, void* dst) {
+  uint64_t mx = 0;
+  for (uint32_t i = 0; i < a.n; i++) mx = a.bytes[i] > mx ? a.bytes[i] : mx;
+  const uint32_t bx = (uint32_t)std::min<uint64_t>(std::max<uint64_t>((mx / 4 + TPB - 1) / TPB, 1), 64);
+  LAUNCH(prof, "gather", s, 0.0,
+         hipLaunchKernelGGL(k_pack, dim3(bx, a.n), dim3(TPB), 0, s, a, reinterpret_cast<uint32_t*>(dst)));
 }
 
 void launch_fri_remainder(Prof& prof, hipStream_t s, const felt* E, uint32_t logB, uint32_t m, felt off_inv,

@@ -358,11 +358,26 @@ void fetch_all(zkp_ctx* ctx, const std::vector<Fetch>& fs) {
   size_t tot = 0;
   for (const Fetch& f : fs) tot += (f.bytes + 15) & ~(size_t)15;
   uint8_t* hp = (uint8_t*)ctx->pinned(tot + 16);
+  uint8_t* stage = ctx->buf<uint8_t>("fetch_stage", tot + 16);
+  // pack the segments on the device (k_pack, PACK_MAX per launch), then one D2H copy
   size_t o = 0;
+  PackArgs pa{};
+  auto flush = [&] {
+    if (pa.n) launch_pack(ctx->prof, ctx->stream, pa, stage);
+    pa.n = 0;
+  };
   for (const Fetch& f : fs) {
-    if (f.bytes) HIP_CHECK(hipMemcpyAsync(hp + o, f.dev, f.bytes, hipMemcpyDeviceToHost, ctx->stream));
+    if (f.bytes % 4) throw ZkpFail{ZKP_ERR_ARGUMENT, "fetch of a non-word-sized segment"};
+    if (f.bytes) {
+      pa.src[pa.n] = f.dev;
+      pa.bytes[pa.n] = f.bytes;
+      pa.off[pa.n] = o;
+      if (++pa.n == PACK_MAX) flush();
+    }
     o += (f.bytes + 15) & ~(size_t)15;
   }
+  flush();
+  HIP_CHECK(hipMemcpyAsync(hp, stage, tot, hipMemcpyDeviceToHost, ctx->stream));
   ctx->sync();
   o = 0;
   for (const Fetch& f : fs) {
@@ -456,8 +471,11 @@ int prove_impl(zkp_ctx* ctx, zkp_comm* cm, int air_id, const felt* d_trace, uint
   ctx->ensure_coset(logn, logB, logce);
   const felt* Sj0 = ctx->S(logn, logB) + (uint64_t)j0 * n;
   // domain points: coset offsets g*w_N^j (LDE cosets) and g*w_M^u (CE cosets), w_n^t table
-  felt* cx = ctx->buf<felt>("coset_x", B + ce);
-  {
+  // (domain-only: cached per (n, B, ce), so no upload sits between the proof's kernels)
+  const std::string cxkey = "coset_x_" + std::to_string(logn) + "_" + std::to_string(logB) + "_" +
+                            std::to_string(logce);
+  felt* cx = ctx->buf<felt>(cxkey, B + ce);
+  if (!ctx->have_cached(cxkey)) {
     std::vector<felt> h(B + ce);
     felt wN = root_of_unity(logN), wM = root_of_unity(logn + logce);
     for (uint32_t j = 0; j < B; j++) h[j] = mul(g, pow_u64(wN, j));
@@ -596,20 +614,25 @@ int prove_impl(zkp_ctx* ctx, zkp_comm* cm, int air_id, const felt* d_trace, uint
       cm->all_to_all(st, send, recv, (size_t)celmax * nR * 16);
     }
     // coefs[u*C + m] = w_ce^-um * g^-mn / ce ; blk[u] = receive block holding CE coset u
-    std::vector<felt> dc((size_t)ce * C);
-    felt wce_inv = inv(root_of_unity(logce)), ce_inv = inv(felt_u64(ce)), gn_inv = inv(pow_u64(g, n));
-    for (uint32_t u = 0; u < ce; u++)
-      for (uint32_t m = 0; m < C; m++)
-        dc[(size_t)u * C + m] = mul(mul(pow_u64(wce_inv, (uint64_t)u * m), pow_u64(gn_inv, m)), ce_inv);
-    std::vector<uint32_t> blk(ce);
-    for (uint32_t u = 0; u < ce; u++) {
-      uint32_t s = ce_owner(u);
-      blk[u] = s * celmax + (u - ce_first(s));
+    // (shape-only: cached per (n, ce, C, R, celmax))
+    const std::string dkey = "comp_dft_" + std::to_string(logn) + "_" + std::to_string(logce) + "_" +
+                             std::to_string(C) + "_" + std::to_string(R) + "_" + std::to_string(celmax);
+    felt* dcoefs = ctx->buf<felt>(dkey + "_coefs", (size_t)ce * C);
+    uint32_t* dblk = ctx->buf<uint32_t>(dkey + "_blk", ce);
+    if (!ctx->have_cached(dkey)) {
+      std::vector<felt> dc((size_t)ce * C);
+      felt wce_inv = inv(root_of_unity(logce)), ce_inv = inv(felt_u64(ce)), gn_inv = inv(pow_u64(g, n));
+      for (uint32_t u = 0; u < ce; u++)
+        for (uint32_t m = 0; m < C; m++)
+          dc[(size_t)u * C + m] = mul(mul(pow_u64(wce_inv, (uint64_t)u * m), pow_u64(gn_inv, m)), ce_inv);
+      std::vector<uint32_t> blk(ce);
+      for (uint32_t u = 0; u < ce; u++) {
+        uint32_t s = ce_owner(u);
+        blk[u] = s * celmax + (u - ce_first(s));
+      }
+      ctx->upload(dcoefs, dc.data(), dc.size() * 16);
+      ctx->upload(dblk, blk.data(), blk.size() * 4);
     }
-    felt* dcoefs = ctx->buf<felt>("comp_dft_coefs", dc.size());
-    uint32_t* dblk = ctx->buf<uint32_t>("comp_dft_blk", ce);
-    ctx->upload(dcoefs, dc.data(), dc.size() * 16);
-    ctx->upload(dblk, blk.data(), blk.size() * 4);
     felt* slice = R > 1 ? ctx->buf<felt>("comp_ag_send", (size_t)C * nR) : acoef;
     launch_comp_dft(pf, st, recv, dblk, ctx->Si(logn, logB, logce), dcoefs, ce, C, logn, p0, nR, slice);
     if (R > 1) {
@@ -694,13 +717,15 @@ int prove_impl(zkp_ctx* ctx, zkp_comm* cm, int air_id, const felt* d_trace, uint
     uint64_t tot_e = 0, D = N;
     for (uint32_t l = 0; l < L; l++) { tot_e += D / F; D /= F; }
     felt* fe = ctx->buf<felt>("fri_evals", tot_e + 1);
-    std::vector<felt> eps(9);
-    felt einv = inv(root_of_unity(4));
-    eps[0] = one();
-    for (int m = 1; m < 8; m++) eps[m] = mul(eps[m - 1], einv);
-    eps[8] = inv(felt_u64(16));
     felt* deps = ctx->buf<felt>("eps_inv", 9);
-    ctx->upload(deps, eps.data(), 9 * 16);
+    if (!ctx->have_cached("eps_inv")) {  // constants of the fold-16 iDFT
+      std::vector<felt> eps(9);
+      felt einv = inv(root_of_unity(4));
+      eps[0] = one();
+      for (int m = 1; m < 8; m++) eps[m] = mul(eps[m - 1], einv);
+      eps[8] = inv(felt_u64(16));
+      ctx->upload(deps, eps.data(), 9 * 16);
+    }
     felt* E = deep;
     uint64_t m = n, eo = 0;
     uint32_t Bc = Bl, jc = j0;

@@ -83,6 +83,14 @@ void launch_merkle_from_shards(Prof& prof, hipStream_t s, const uint32_t* recv, 
                                uint32_t* nodes);
 // internal nodes nodes[1..L) from leaves nodes[L..2L)
 void launch_merkle_tree(Prof& prof, hipStream_t s, uint32_t* nodes, uint64_t L);
+constexpr uint32_t PACK_MAX = 16;
+struct PackArgs {
+  const void* src[PACK_MAX];
+  uint64_t bytes[PACK_MAX], off[PACK_MAX];
+  uint32_t n;
+};
+// dst[off[i] ..) = src[i][0 .. bytes[i]) for i < n (byte counts multiples of 4)
+void launch_pack(Prof& prof, hipStream_t s, const PackArgs& a, void* dst);
 // seed from host words, or (seed_words == nullptr) from the device coin state seed_dev
 void launch_grind(Prof& prof, hipStream_t s, const uint32_t* seed_words, const uint32_t* seed_dev, uint64_t base,
                   uint64_t count, uint32_t bits, unsigned long long* result);
