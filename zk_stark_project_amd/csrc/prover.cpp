@@ -911,6 +911,9 @@ int prove_impl(zkp_ctx* ctx, zkp_comm* cm, int air_id, const felt* d_trace, uint
   auto row_owner = [&](uint64_t j) -> uint32_t { return R > 1 ? (uint32_t)(j / Bl) : 0; };
   auto lde_values = [&](const felt* src, uint32_t cols) {
     SegPlan sp{src, {}, {}, {}, 4};
+    sp.idx.reserve(pos.size() * cols);
+    sp.owner.reserve(pos.size() * cols);
+    sp.host_dig.reserve(pos.size() * cols);
     for (uint64_t p : pos) {
       uint64_t j = p & (B - 1), t = p >> logB;
       uint32_t ow = row_owner(j);
@@ -939,7 +942,8 @@ int prove_impl(zkp_ctx* ctx, zkp_comm* cm, int air_id, const felt* d_trace, uint
       }
     return sp;
   };
-  BatchPlan bt = plan_batch(N, pos), bc = plan_batch(N, pos);
+  const BatchPlan bt = plan_batch(N, pos);
+  const BatchPlan& bc = bt;  // the constraint tree has the same shape and positions
   std::vector<std::vector<uint64_t>> fpos(L);
   std::vector<BatchPlan> bf(L);
   std::vector<SegPlan> plan;
@@ -1019,28 +1023,32 @@ int prove_impl(zkp_ctx* ctx, zkp_comm* cm, int air_id, const felt* d_trace, uint
     }
   }
   size_t seg_cursor = 0;
-  auto next_vals = [&]() {
+  // values and batch paths are written straight from the gathered words
+  // (felts are stored canonical LE, i.e. already in their wire format)
+  auto write_values = [&](Writer& wr) {
     const GatherSeg& gs = segs[seg_cursor++];
-    std::vector<felt> v(gs.count);
-    memcpy(v.data(), gathered.data() + gs.out_off, gs.count * 16);
-    return v;
+    wr.u32((uint32_t)(gs.count * 16));
+    wr.put(gathered.data() + gs.out_off, gs.count * 16);
   };
-  auto next_digests = [&]() {
+  auto write_batch = [&](Writer& wr, const BatchPlan& bp) {
     const GatherSeg& gs = segs[seg_cursor++];
-    return std::vector<uint32_t>(gathered.begin() + gs.out_off, gathered.begin() + gs.out_off + gs.count * 8);
-  };
-  auto write_batch = [&](Writer& wr, const BatchPlan& bp, const std::vector<uint32_t>& d) {
+    const uint32_t* d = gathered.data() + gs.out_off;
+    size_t nodes = 0;
+    for (auto& p : bp.paths) nodes += p.size();
+    wr.u32((uint32_t)(2 + bp.paths.size() + 32 * nodes));
     wr.u8((uint8_t)bp.depth);
     wr.u8((uint8_t)bp.paths.size());
     size_t k = 0;
     for (auto& p : bp.paths) {
       wr.u8((uint8_t)p.size());
-      for (size_t i = 0; i < p.size(); i++, k++) wr.put(d.data() + 8 * k, 32);
+      wr.put(d + 8 * k, 32 * p.size());
+      k += p.size();
     }
   };
 
   // 10. serialize (≙ Proof::to_bytes)
   Writer wr;
+  wr.b.reserve((size_t)out_words * 4 + 64 * (size_t)(L + 4) + 32 * (size_t)(w + C) + 16 * remainder.size() + 4096);
   write_context(wr, air, o);
   wr.u8((uint8_t)np);
   wr.u16((uint16_t)(32 * (2 + L + 1)));
@@ -1050,13 +1058,8 @@ int prove_impl(zkp_ctx* ctx, zkp_comm* cm, int air_id, const felt* d_trace, uint
   wr.put(T.remainder_commitment, 32);
   wr.u8(1);
   for (int seg = 0; seg < 2; seg++) {
-    std::vector<felt> vals = next_vals();
-    std::vector<uint32_t> dig = next_digests();
-    Writer vw, pw;
-    for (felt v : vals) vw.fe(v);
-    write_batch(pw, seg == 0 ? bt : bc, dig);
-    wr.u32((uint32_t)vw.b.size()); wr.put(vw.b.data(), vw.b.size());
-    wr.u32((uint32_t)pw.b.size()); wr.put(pw.b.data(), pw.b.size());
+    write_values(wr);
+    write_batch(wr, seg == 0 ? bt : bc);
   }
   wr.u16((uint16_t)(1 + 16 * 2 * w));
   wr.u8(2);
@@ -1065,13 +1068,8 @@ int prove_impl(zkp_ctx* ctx, zkp_comm* cm, int air_id, const felt* d_trace, uint
   for (felt v : ood_comp) wr.fe(v);
   wr.u8((uint8_t)L);
   for (uint32_t l = 0; l < L; l++) {
-    std::vector<felt> vals = next_vals();
-    std::vector<uint32_t> dig = next_digests();
-    Writer vw, pw;
-    for (felt v : vals) vw.fe(v);
-    write_batch(pw, bf[l], dig);
-    wr.u32((uint32_t)vw.b.size()); wr.put(vw.b.data(), vw.b.size());
-    wr.u32((uint32_t)pw.b.size()); wr.put(pw.b.data(), pw.b.size());
+    write_values(wr);
+    write_batch(wr, bf[l]);
   }
   wr.u16((uint16_t)(16 * remainder.size()));
   for (felt v : remainder) wr.fe(v);
