@@ -550,6 +550,7 @@ struct MerkleArgs {
   uint64_t R;       // MODE 1: rows per coset (m/16)
   uint32_t* nodes;
   uint64_t L;       // leaves of this (sub)tree level
+  MerkleTail tail;  // k_merkle_fused: finish the tree (+ FRI coin step) in the last block
 };
 
 template <int MODE>
@@ -575,6 +576,9 @@ __device__ __forceinline__ void merge8(const uint32_t l[8], const uint32_t r[8],
   b3::set_iv(out);
   b3::compress(out, m, 0, 64, b3::CHUNK_START | b3::CHUNK_END | b3::ROOT);
 }
+
+__device__ void coin_fri_step(uint32_t* __restrict__ seed, const uint32_t* root, felt* __restrict__ alpha_out,
+                              uint32_t* __restrict__ root_out);
 
 template <int MODE>
 __global__ __launch_bounds__(256) void k_merkle_fused(MerkleArgs a) {
@@ -614,6 +618,54 @@ __global__ __launch_bounds__(256) void k_merkle_fused(MerkleArgs a) {
 #pragma unroll
       for (int i = 0; i < 8; i++) sd[t * 9 + i] = o[i];
       store_digest(a.nodes + (lvl + lbase + t) * 8, o);
+    }
+  }
+  if (!a.tail.done) return;
+  // the last block to finish builds the levels above the G = gridDim.x subtree
+  // roots (nodes[G .. 2G), G <= 512) up to nodes[1], then runs the FRI coin step
+  // (release: fence + counter; acquire: fence after seeing the count)
+  __shared__ int s_last;
+  __threadfence();
+  __syncthreads();
+  if (t == 0) s_last = atomicAdd(a.tail.done, 1u) == gridDim.x - 1;
+  __syncthreads();
+  if (!s_last) return;
+  __threadfence();
+  const uint32_t G = gridDim.x;
+  if (G > 1) {
+    for (uint32_t i = t; i < G / 2; i += 256) {  // level G/2 from the roots in global memory
+      uint32_t l[8], r[8], o[8];
+      load_digest(a.nodes + (uint64_t)(G + 2 * i) * 8, l);
+      load_digest(a.nodes + (uint64_t)(G + 2 * i + 1) * 8, r);
+      merge8(l, r, o);
+      store_digest(a.nodes + (uint64_t)(G / 2 + i) * 8, o);
+#pragma unroll
+      for (int k = 0; k < 8; k++) sd[i * 9 + k] = o[k];
+    }
+    for (uint32_t sl = G / 4; sl >= 1; sl >>= 1) {
+      __syncthreads();
+      uint32_t o[8];
+      if (t < sl) {
+        uint32_t l[8], r[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) { l[k] = sd[(2 * t) * 9 + k]; r[k] = sd[(2 * t + 1) * 9 + k]; }
+        merge8(l, r, o);
+      }
+      __syncthreads();
+      if (t < sl) {
+#pragma unroll
+        for (int k = 0; k < 8; k++) sd[t * 9 + k] = o[k];
+        store_digest(a.nodes + (uint64_t)(sl + t) * 8, o);
+      }
+    }
+  }
+  __syncthreads();
+  if (t == 0) {
+    *a.tail.done = 0;  // ready for the next launch on this stream
+    if (a.tail.coin_seed) {
+      uint32_t root[8];
+      load_digest(a.nodes + 8, root);
+      coin_fri_step(a.tail.coin_seed, root, a.tail.alpha_out, a.tail.root_out);
     }
   }
 }
@@ -961,9 +1013,10 @@ __global__ void k_dt_draw_z(uint32_t* __restrict__ seed, const uint32_t* __restr
   }
 }
 
-__global__ void k_coin_fri_layer(uint32_t* __restrict__ seed, const uint32_t* __restrict__ root,
-                                 felt* __restrict__ alpha_out, uint32_t* __restrict__ root_out) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+// FRI commit-loop Fiat-Shamir step (one thread): seed <- BLAKE3(seed || root),
+// alpha = first draw < p; root copied to root_out
+__device__ void coin_fri_step(uint32_t* __restrict__ seed, const uint32_t* root, felt* __restrict__ alpha_out,
+                              uint32_t* __restrict__ root_out) {
   uint32_t m[16], s[8];
   for (int i = 0; i < 8; i++) { m[i] = seed[i]; m[8 + i] = root[i]; root_out[i] = root[i]; }
   b3::set_iv(s);
@@ -982,6 +1035,12 @@ __global__ void k_coin_fri_layer(uint32_t* __restrict__ seed, const uint32_t* __
   }
   *alpha_out = a;
   for (int i = 0; i < 8; i++) seed[i] = s[i];
+}
+
+__global__ void k_coin_fri_layer(uint32_t* __restrict__ seed, const uint32_t* __restrict__ root,
+                                 felt* __restrict__ alpha_out, uint32_t* __restrict__ root_out) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  coin_fri_step(seed, root, alpha_out, root_out);
 }
 
 struct SeedArg {
@@ -1936,7 +1995,7 @@ static void merkle_pass(Prof& prof, hipStream_t s, const MerkleArgs& a, uint32_t
 
 // upper levels: wide levels by lane passes (4 levels each), the narrow top by
 // the LDS-fused kernel (9 levels per launch, parallel tail)
-void merkle_upper(Prof& prof, hipStream_t s, uint32_t* nodes, uint64_t L) {
+bool merkle_upper(Prof& prof, hipStream_t s, uint32_t* nodes, uint64_t L, const MerkleTail* tail) {
   while (L > 1) {
     MerkleArgs a{};
     a.nodes = nodes;
@@ -1949,15 +2008,19 @@ void merkle_upper(Prof& prof, hipStream_t s, uint32_t* nodes, uint64_t L) {
       L >>= 4;
     } else {
       uint64_t blocks = (L + 511) / 512;
+      const bool finish = tail && tail->done && blocks <= 512;  // this launch completes the tree
+      if (finish) a.tail = *tail;
       LAUNCH(prof, "merkle_top9", s, (double)L * 64.0,
              hipLaunchKernelGGL(k_merkle_fused<2>, dim3((uint32_t)blocks), dim3(256), 0, s, a));
+      if (finish) return true;
       L = L >= 512 ? L / 512 : 1;
     }
   }
+  return false;
 }
 
-void launch_merkle_lde(Prof& prof, hipStream_t s, const felt* lde, uint32_t cols, uint32_t logB, uint64_t n,
-                       uint32_t* nodes, uint64_t L) {
+bool launch_merkle_lde(Prof& prof, hipStream_t s, const felt* lde, uint32_t cols, uint32_t logB, uint64_t n,
+                       uint32_t* nodes, uint64_t L, const MerkleTail* tail) {
   MerkleArgs a{};
   a.src = lde;
   a.n = n;
@@ -1968,11 +2031,11 @@ void launch_merkle_lde(Prof& prof, hipStream_t s, const felt* lde, uint32_t cols
   uint32_t H = 0;
   while (H < 3 && (1ull << (H + 1)) <= L) H++;
   merkle_pass<0>(prof, s, a, H, "merkle_lde", (double)L * (cols * 16.0 + 64.0));
-  merkle_upper(prof, s, nodes, L >> H);
+  return merkle_upper(prof, s, nodes, L >> H, tail);
 }
 
-void launch_merkle_fri(Prof& prof, hipStream_t s, const felt* E, uint64_t m16, uint32_t logB, uint32_t F,
-                       uint32_t* nodes) {
+bool launch_merkle_fri(Prof& prof, hipStream_t s, const felt* E, uint64_t m16, uint32_t logB, uint32_t F,
+                       uint32_t* nodes, const MerkleTail* tail) {
   const uint64_t R = m16 << logB;
   MerkleArgs a{};
   a.src = E;
@@ -1985,15 +2048,17 @@ void launch_merkle_fri(Prof& prof, hipStream_t s, const felt* E, uint64_t m16, u
     // small layers: a lane subtree would serialise 19 compressions per lane on a
     // few waves; hash 2 rows per thread and build 9 levels per block instead
     uint64_t blocks = (R + 511) / 512;
+    const bool finish = tail && tail->done && blocks <= 512;
+    if (finish) a.tail = *tail;
     LAUNCH(prof, "merkle_fri", s, (double)R * (F * 16.0 + 64.0),
            hipLaunchKernelGGL(k_merkle_fused<1>, dim3((uint32_t)blocks), dim3(256), 0, s, a));
-    merkle_upper(prof, s, nodes, R >= 512 ? R / 512 : 1);
-    return;
+    if (finish) return true;
+    return merkle_upper(prof, s, nodes, R >= 512 ? R / 512 : 1, tail);
   }
   uint32_t H = 0;
   while (H < 2 && (1ull << (H + 1)) <= R) H++;
   merkle_pass<1>(prof, s, a, H, "merkle_fri", (double)R * (F * 16.0 + 64.0));
-  merkle_upper(prof, s, nodes, R >> H);
+  return merkle_upper(prof, s, nodes, R >> H, tail);
 }
 
 void launch_leaf_hash_lde(Prof& prof, hipStream_t s, const felt* lde, uint32_t cols, uint32_t logB, uint64_t n,
@@ -2148,7 +2213,7 @@ void launch_merkle_from_shards(Prof& prof, hipStream_t s, const uint32_t* recv, 
   const uint64_t L = 1ull << (logB + logrr);
   LAUNCH(prof, "leaf_unpack", s, (double)L * 64.0,
          hipLaunchKernelGGL(k_leaf_unpack, dim3(blocks_for(L)), dim3(TPB), 0, s, recv, logB, logrr, nodes, L));
-  merkle_upper(prof, s, nodes, L);
+  merkle_upper(prof, s, nodes, L, nullptr);
 }
 
 void launch_comp_dft(Prof& prof, hipStream_t s, const felt* recv, const uint32_t* blk, const felt* Si,

@@ -306,9 +306,12 @@ struct TreeShard {
 // commit the rows of a coset-major source held by this rank (cosets [j0, j0+Bl)):
 // mode 0 = LDE rows (cols columns, n rows per coset), mode 1 = FRI rows (16
 // values, 2^logrows rows per coset). Unsharded sources hold all B cosets.
-void commit_rows(zkp_ctx* ctx, zkp_comm* cm, int mode, const felt* src, uint64_t n, uint32_t cols, uint32_t logB,
+// Unsharded trees finish in the last block of their top launch (MerkleTail);
+// with coin (FRI layers) that block also runs the layer's coin step, and the
+// function returns true when it did.
+bool commit_rows(zkp_ctx* ctx, zkp_comm* cm, int mode, const felt* src, uint64_t n, uint32_t cols, uint32_t logB,
                  uint32_t logrows, bool sharded, const std::string& name, TreeShard& tr, uint8_t root[32],
-                 bool fetch_root = true) {
+                 bool fetch_root = true, const MerkleTail* coin = nullptr) {
   Prof& pf = ctx->prof;
   hipStream_t st = ctx->stream;
   const uint64_t L = 1ull << (logB + logrows);
@@ -316,14 +319,18 @@ void commit_rows(zkp_ctx* ctx, zkp_comm* cm, int mode, const felt* src, uint64_t
     tr.logR = 0;
     tr.Lr = L;
     tr.nodes = ctx->buf<uint32_t>(name, (size_t)16 * L);
-    if (mode == 0) launch_merkle_lde(pf, st, src, cols, logB, n, tr.nodes, L);
-    else launch_merkle_fri(pf, st, src, 1ull << logrows, logB, 16, tr.nodes);
+    uint32_t* done = ctx->buf<uint32_t>("merkle_done", 1);
+    if (!ctx->have_cached("merkle_done")) HIP_CHECK(hipMemsetAsync(done, 0, 4, st));
+    MerkleTail tail{done, nullptr, nullptr, nullptr};
+    if (coin) { tail.coin_seed = coin->coin_seed; tail.alpha_out = coin->alpha_out; tail.root_out = coin->root_out; }
+    bool ran = mode == 0 ? launch_merkle_lde(pf, st, src, cols, logB, n, tr.nodes, L, &tail)
+                         : launch_merkle_fri(pf, st, src, 1ull << logrows, logB, 16, tr.nodes, &tail);
     tr.top.assign(2, {});
     if (fetch_root) {  // otherwise the caller reads nodes[1] later
       ctx->download(root, tr.nodes + 8, 32);
       memcpy(tr.top[1].data(), root, 32);
     }
-    return;
+    return ran && coin;
   }
   const uint32_t R = cm->world, logR = ilog2(R), logBl = logB - logR;
   const uint32_t logrr = logrows - logR;
@@ -343,6 +350,7 @@ void commit_rows(zkp_ctx* ctx, zkp_comm* cm, int mode, const felt* src, uint64_t
   for (uint32_t s = 0; s < R; s++) memcpy(tr.top[R + s].data(), hr.data() + 32 * s, 32);
   for (uint32_t k = R - 1; k >= 1; k--) merge_bytes(tr.top[2 * k].data(), tr.top[2 * k + 1].data(), tr.top[k].data());
   memcpy(root, tr.top[1].data(), 32);
+  return false;
 }
 
 // evaluate bit-reversed coefficient arrays (scaled by n) at x0, x1 -> values (x n^-1)
@@ -752,15 +760,18 @@ int prove_impl(zkp_ctx* ctx, zkp_comm* cm, int air_id, const felt* d_trace, uint
       Layer& ly = layers[l];
       ly.E = E; ly.m = m; ly.Bc = Bc; ly.jc = jc; ly.sharded = sh;
       // sharded layers assemble the root on the host (top levels); it is staged back for the coin
-      commit_rows(ctx, cm, 1, E, 0, F, logB, ilog2(m16), sh, "ftree_" + std::to_string(l), ly.tree,
-                  T.fri_roots[l], /*fetch_root=*/sh);
-      const uint32_t* root_src = ly.tree.nodes + 8;
-      if (sh) {
-        uint32_t* staged = roots_d + 8 * (size_t)L;  // scratch slot
-        ctx->upload(staged, T.fri_roots[l], 32);
-        root_src = staged;
+      const MerkleTail coin{nullptr, coin_d, alphas_d + l, roots_d + 8 * (size_t)l};
+      const bool coin_done = commit_rows(ctx, cm, 1, E, 0, F, logB, ilog2(m16), sh, "ftree_" + std::to_string(l),
+                                         ly.tree, T.fri_roots[l], /*fetch_root=*/sh, &coin);
+      if (!coin_done) {
+        const uint32_t* root_src = ly.tree.nodes + 8;
+        if (sh) {
+          uint32_t* staged = roots_d + 8 * (size_t)L;  // scratch slot
+          ctx->upload(staged, T.fri_roots[l], 32);
+          root_src = staged;
+        }
+        launch_coin_fri_layer(pf, st, coin_d, root_src, alphas_d + l, roots_d + 8 * (size_t)l);
       }
-      launch_coin_fri_layer(pf, st, coin_d, root_src, alphas_d + l, roots_d + 8 * (size_t)l);
       felt* nxt = fe + eo;
       launch_fri_fold(pf, st, E, m16, Bc, jc, logB, F, alphas_d + l, inv(off), ctx->itws(logN), ilog2(D), deps,
                       nxt);

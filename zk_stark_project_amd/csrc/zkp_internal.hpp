@@ -67,13 +67,23 @@ void launch_leaf_hash_lde(Prof& prof, hipStream_t s, const felt* lde, uint32_t c
 // leaves of FRI layer: row r = [E[r + k*R] for k < F] -> nodes[R + r]
 void launch_leaf_hash_fri(Prof& prof, hipStream_t s, const felt* E, uint64_t R, uint32_t F, uint32_t* nodes);
 // fused builders: leaves + all levels (nodes[1..2L)) in ceil(log2(L)/9) launches
-void launch_merkle_lde(Prof& prof, hipStream_t s, const felt* lde, uint32_t cols, uint32_t logB, uint64_t n,
-                       uint32_t* nodes, uint64_t L);
+// Optional tree tail: with done (a zeroed per-stream counter) the launch that
+// produces the top subtree roots also finishes the tree in its last block and,
+// with coin_seed, runs the FRI coin step (seed <- H(seed || root), alpha_out,
+// root_out). The launchers return true when the tail ran.
+struct MerkleTail {
+  uint32_t* done;
+  uint32_t* coin_seed;
+  felt* alpha_out;
+  uint32_t* root_out;
+};
+bool launch_merkle_lde(Prof& prof, hipStream_t s, const felt* lde, uint32_t cols, uint32_t logB, uint64_t n,
+                       uint32_t* nodes, uint64_t L, const MerkleTail* tail = nullptr);
 // FRI layer tree over coset-major evaluations (B cosets of 16*m16): leaf r = j + B*t'
-void launch_merkle_fri(Prof& prof, hipStream_t s, const felt* E, uint64_t m16, uint32_t logB, uint32_t F,
-                       uint32_t* nodes);
+bool launch_merkle_fri(Prof& prof, hipStream_t s, const felt* E, uint64_t m16, uint32_t logB, uint32_t F,
+                       uint32_t* nodes, const MerkleTail* tail = nullptr);
 // nodes[1..L) from leaf digests already in nodes[L..2L)
-void merkle_upper(Prof& prof, hipStream_t s, uint32_t* nodes, uint64_t L);
+bool merkle_upper(Prof& prof, hipStream_t s, uint32_t* nodes, uint64_t L, const MerkleTail* tail = nullptr);
 // sharded commitments: hash the shard's rows (mode 0: LDE rows of cols columns;
 // mode 1: FRI rows of 16) into per-destination blocks; then, after the
 // all-to-all, rebuild the natural-order leaves of this rank's range and its subtree
