@@ -577,8 +577,7 @@ __device__ __forceinline__ void merge8(const uint32_t l[8], const uint32_t r[8],
   b3::compress(out, m, 0, 64, b3::CHUNK_START | b3::CHUNK_END | b3::ROOT);
 }
 
-__device__ void coin_fri_step(uint32_t* __restrict__ seed, const uint32_t* root, felt* __restrict__ alpha_out,
-                              uint32_t* __restrict__ root_out);
+__device__ void merkle_tail_op(const MerkleTail& tl, const uint32_t* root);
 
 template <int MODE>
 __global__ __launch_bounds__(256) void k_merkle_fused(MerkleArgs a) {
@@ -660,14 +659,8 @@ __global__ __launch_bounds__(256) void k_merkle_fused(MerkleArgs a) {
     }
   }
   __syncthreads();
-  if (t == 0) {
-    *a.tail.done = 0;  // ready for the next launch on this stream
-    if (a.tail.coin_seed) {
-      uint32_t root[8];
-      load_digest(a.nodes + 8, root);
-      coin_fri_step(a.tail.coin_seed, root, a.tail.alpha_out, a.tail.root_out);
-    }
-  }
+  if (t == 0) *a.tail.done = 0;  // ready for the next launch on this stream
+  if (a.tail.op != MERKLE_TAIL_NONE) merkle_tail_op(a.tail, a.nodes + 8);  // whole block
 }
 
 // Lane-subtree Merkle build: every lane turns 2^H consecutive leaves into their
@@ -926,8 +919,8 @@ __global__ __launch_bounds__(64) void k_dt_deep_coeffs(uint32_t* __restrict__ se
 // (ConstraintCompositionCoefficients::draw: Linear = n draws, Algebraic = powers
 // of one draw, Horner = the powers reversed). One block; Linear draws run in
 // parallel with a sequential redo if any candidate was rejected.
-__global__ __launch_bounds__(TPB) void k_dt_draw_coeffs(uint32_t* __restrict__ seed, const uint32_t* __restrict__ root,
-                                                        uint32_t method, uint32_t ncoef, felt* __restrict__ cc) {
+__device__ void dt_draw_coeffs_block(uint32_t* __restrict__ seed, const uint32_t* __restrict__ root, uint32_t method,
+                                     uint32_t ncoef, felt* __restrict__ cc) {
   __shared__ uint32_t s[8];
   __shared__ felt s_alpha;
   __shared__ int s_rej;
@@ -941,6 +934,10 @@ __global__ __launch_bounds__(TPB) void k_dt_draw_coeffs(uint32_t* __restrict__ s
   uint32_t t[8];
   for (int i = 0; i < 8; i++) t[i] = s[i];
   dcoin_draw_coeffs_block(t, method, ncoef, cc, &s_alpha, &s_rej);
+}
+__global__ __launch_bounds__(TPB) void k_dt_draw_coeffs(uint32_t* __restrict__ seed, const uint32_t* __restrict__ root,
+                                                        uint32_t method, uint32_t ncoef, felt* __restrict__ cc) {
+  dt_draw_coeffs_block(seed, root, method, ncoef, cc);
 }
 
 // coefficient-dependent constants of the constraint evaluation kernels, from cc:
@@ -992,24 +989,51 @@ __global__ __launch_bounds__(TPB) void k_dt_eval_consts(int air, const felt* __r
 
 // reseed with the constraint root, draw z; zz = (z, z*w_n); pw tables
 // pw[l] = z^(2^l), pw[logn + l] = (z w_n)^(2^l) for the OOD evaluation
+__device__ void dt_draw_z_block(uint32_t* __restrict__ seed, const uint32_t* __restrict__ root, felt wn, uint32_t logn,
+                                felt* __restrict__ zz, felt* __restrict__ pw) {
+  __shared__ felt s_z;
+  if (threadIdx.x == 0) {
+    uint32_t t[8], d[8];
+    for (int i = 0; i < 8; i++) { t[i] = seed[i]; d[i] = root[i]; }
+    dcoin_reseed(t, d);
+    for (int i = 0; i < 8; i++) seed[i] = t[i];
+    uint64_t ctr = 0;
+    const felt z = dcoin_draw(t, &ctr);
+    zz[0] = z;
+    zz[1] = mul(z, wn);
+    s_z = z;
+  }
+  __syncthreads();
+  if (threadIdx.x >= 2) return;
+  // the two squaring chains (z and z*w_n) on two lanes
+  felt a = threadIdx.x == 0 ? s_z : mul(s_z, wn);
+  felt* out = pw + threadIdx.x * logn;
+  for (uint32_t l = 0; l < logn; l++) {
+    out[l] = a;
+    a = sqr(a);
+  }
+}
 __global__ void k_dt_draw_z(uint32_t* __restrict__ seed, const uint32_t* __restrict__ root, felt wn, uint32_t logn,
                             felt* __restrict__ zz, felt* __restrict__ pw) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
-  uint32_t t[8], d[8];
-  for (int i = 0; i < 8; i++) { t[i] = seed[i]; d[i] = root[i]; }
-  dcoin_reseed(t, d);
-  for (int i = 0; i < 8; i++) seed[i] = t[i];
-  uint64_t ctr = 0;
-  felt z = dcoin_draw(t, &ctr);
-  felt zg = mul(z, wn);
-  zz[0] = z;
-  zz[1] = zg;
-  felt a = z, b = zg;
-  for (uint32_t l = 0; l < logn; l++) {
-    pw[l] = a;
-    pw[logn + l] = b;
-    a = sqr(a);
-    b = sqr(b);
+  dt_draw_z_block(seed, root, wn, logn, zz, pw);
+}
+
+__device__ void coin_fri_step(uint32_t* __restrict__ seed, const uint32_t* root, felt* __restrict__ alpha_out,
+                              uint32_t* __restrict__ root_out);
+
+// what the last block of a finished Merkle tree does with its root (all threads
+// of the block call it; root = nodes + 8, written by this block)
+__device__ void merkle_tail_op(const MerkleTail& tl, const uint32_t* root) {
+  if (tl.op == MERKLE_TAIL_FRI_COIN) {
+    if (threadIdx.x == 0) {
+      uint32_t r[8];
+      load_digest(root, r);
+      coin_fri_step(tl.coin_seed, r, tl.alpha_out, tl.root_out);
+    }
+  } else if (tl.op == MERKLE_TAIL_DRAW_COEFFS) {
+    dt_draw_coeffs_block(tl.coin_seed, root, tl.method, tl.ncoef, tl.out);
+  } else if (tl.op == MERKLE_TAIL_DRAW_Z) {
+    dt_draw_z_block(tl.coin_seed, root, tl.wn, tl.logn, tl.out, tl.pw);
   }
 }
 

@@ -321,8 +321,8 @@ bool commit_rows(zkp_ctx* ctx, zkp_comm* cm, int mode, const felt* src, uint64_t
     tr.nodes = ctx->buf<uint32_t>(name, (size_t)16 * L);
     uint32_t* done = ctx->buf<uint32_t>("merkle_done", 1);
     if (!ctx->have_cached("merkle_done")) HIP_CHECK(hipMemsetAsync(done, 0, 4, st));
-    MerkleTail tail{done, nullptr, nullptr, nullptr};
-    if (coin) { tail.coin_seed = coin->coin_seed; tail.alpha_out = coin->alpha_out; tail.root_out = coin->root_out; }
+    MerkleTail tail = coin ? *coin : MerkleTail{};
+    tail.done = done;
     bool ran = mode == 0 ? launch_merkle_lde(pf, st, src, cols, logB, n, tr.nodes, L, &tail)
                          : launch_merkle_fri(pf, st, src, 1ull << logrows, logB, 16, tr.nodes, &tail);
     tr.top.assign(2, {});
@@ -498,12 +498,22 @@ int prove_impl(zkp_ctx* ctx, zkp_comm* cm, int air_id, const felt* d_trace, uint
   felt* coef = ctx->buf<felt>("coef", (size_t)(w + C) * n);
   felt* tlde = ctx->buf<felt>("tlde", (size_t)w * Bl * n);
   TreeShard ttree;
+  bool coeffs_drawn = false;
   {
     NttBatch ib{d_trace, coef, nullptr, n, n, 1, 1, w};
     launch_ntt(pf, st, ib, logn, false, ctx->itws(logN), logN);
     NttBatch lb{coef, tlde, Sj0, n, n, Bl, Bl, w * Bl};
     launch_ntt(pf, st, lb, logn, true, ctx->tws(logN), logN);
-    commit_rows(ctx, cm, 0, tlde, n, w, logB, logn, R > 1, "ttree", ttree, T.trace_root, /*fetch_root=*/R > 1);
+    // unsharded: the tree's last block also reseeds with the root and draws the
+    // composition coefficients (MERKLE_TAIL_DRAW_COEFFS)
+    MerkleTail draw{};
+    draw.op = MERKLE_TAIL_DRAW_COEFFS;
+    draw.coin_seed = dt_seed;
+    draw.method = o->batching_constraints;
+    draw.ncoef = ncoef;
+    draw.out = dt_cc;
+    coeffs_drawn = commit_rows(ctx, cm, 0, tlde, n, w, logB, logn, R > 1, "ttree", ttree, T.trace_root,
+                               /*fetch_root=*/R > 1, &draw);
   }
   const uint32_t* troot_d = ttree.nodes + 8;
   if (R > 1) {  // sharded: the root was assembled on the host from the subtree roots
@@ -513,7 +523,7 @@ int prove_impl(zkp_ctx* ctx, zkp_comm* cm, int air_id, const felt* d_trace, uint
   ctx->stage_end("1_trace_commit");
 
   // 3. constraint composition coefficients (drawn on the device) + evaluation (DefaultConstraintEvaluator)
-  launch_dt_draw_coeffs(pf, st, dt_seed, troot_d, o->batching_constraints, ncoef, dt_cc);
+  if (!coeffs_drawn) launch_dt_draw_coeffs(pf, st, dt_seed, troot_d, o->batching_constraints, ncoef, dt_cc);
   felt* comp = ctx->buf<felt>("comp", (size_t)(cel ? cel : 1) * n);
   if (cel) {
     felt wn = root_of_unity(logn);
@@ -604,6 +614,8 @@ int prove_impl(zkp_ctx* ctx, zkp_comm* cm, int air_id, const felt* d_trace, uint
   felt* acoef = coef + (size_t)w * n;
   felt* clde = ctx->buf<felt>("clde", (size_t)C * Bl * n);
   TreeShard ctree;
+  bool z_drawn = false;
+  const felt wn_root = root_of_unity(logn);
   {
     // this rank's slice of bit-reversed coefficient positions: [p0, p0 + nR)
     const uint64_t nR = n >> logR, p0 = (uint64_t)rank * nR;
@@ -652,16 +664,22 @@ int prove_impl(zkp_ctx* ctx, zkp_comm* cm, int air_id, const felt* d_trace, uint
     }
     NttBatch lb{acoef, clde, Sj0, n, n, Bl, Bl, C * Bl};
     launch_ntt(pf, st, lb, logn, true, ctx->tws(logN), logN);
-    commit_rows(ctx, cm, 0, clde, n, C, logB, logn, R > 1, "ctree", ctree, T.constraint_root,
-                /*fetch_root=*/R > 1);
+    MerkleTail draw{};  // unsharded: the tree's last block draws z (MERKLE_TAIL_DRAW_Z)
+    draw.op = MERKLE_TAIL_DRAW_Z;
+    draw.coin_seed = dt_seed;
+    draw.wn = wn_root;
+    draw.logn = logn;
+    draw.out = dt_zz;
+    draw.pw = dt_pw;
+    z_drawn = commit_rows(ctx, cm, 0, clde, n, C, logB, logn, R > 1, "ctree", ctree, T.constraint_root,
+                          /*fetch_root=*/R > 1, &draw);
   }
   const uint32_t* croot_d = ctree.nodes + 8;
   if (R > 1) {
     ctx->upload(dt_roots + 8, T.constraint_root, 32);
     croot_d = dt_roots + 8;
   }
-  const felt wn_root = root_of_unity(logn);
-  launch_dt_draw_z(pf, st, dt_seed, croot_d, wn_root, logn, dt_zz, dt_pw);
+  if (!z_drawn) launch_dt_draw_z(pf, st, dt_seed, croot_d, wn_root, logn, dt_zz, dt_pw);
   ctx->stage_end("2_constraints_commit");
 
   // 5. OOD frame (every rank holds all trace and composition coefficients)
@@ -760,7 +778,11 @@ int prove_impl(zkp_ctx* ctx, zkp_comm* cm, int air_id, const felt* d_trace, uint
       Layer& ly = layers[l];
       ly.E = E; ly.m = m; ly.Bc = Bc; ly.jc = jc; ly.sharded = sh;
       // sharded layers assemble the root on the host (top levels); it is staged back for the coin
-      const MerkleTail coin{nullptr, coin_d, alphas_d + l, roots_d + 8 * (size_t)l};
+      MerkleTail coin{};
+      coin.op = MERKLE_TAIL_FRI_COIN;
+      coin.coin_seed = coin_d;
+      coin.alpha_out = alphas_d + l;
+      coin.root_out = roots_d + 8 * (size_t)l;
       const bool coin_done = commit_rows(ctx, cm, 1, E, 0, F, logB, ilog2(m16), sh, "ftree_" + std::to_string(l),
                                          ly.tree, T.fri_roots[l], /*fetch_root=*/sh, &coin);
       if (!coin_done) {

@@ -71,11 +71,20 @@ void launch_leaf_hash_fri(Prof& prof, hipStream_t s, const felt* E, uint64_t R, 
 // produces the top subtree roots also finishes the tree in its last block and,
 // with coin_seed, runs the FRI coin step (seed <- H(seed || root), alpha_out,
 // root_out). The launchers return true when the tail ran.
+// op: what the last block does with the root (coin state in coin_seed):
+//   MERKLE_TAIL_FRI_COIN    reseed, draw alpha -> alpha_out, root -> root_out
+//   MERKLE_TAIL_DRAW_COEFFS reseed, draw ncoef composition coefficients -> out
+//   MERKLE_TAIL_DRAW_Z      reseed, draw z -> out = (z, z wn), pw tables (logn each)
+enum { MERKLE_TAIL_NONE = 0, MERKLE_TAIL_FRI_COIN = 1, MERKLE_TAIL_DRAW_COEFFS = 2, MERKLE_TAIL_DRAW_Z = 3 };
 struct MerkleTail {
   uint32_t* done;
   uint32_t* coin_seed;
   felt* alpha_out;
   uint32_t* root_out;
+  uint32_t op, method, ncoef, logn;
+  felt wn;
+  felt* out;
+  felt* pw;
 };
 bool launch_merkle_lde(Prof& prof, hipStream_t s, const felt* lde, uint32_t cols, uint32_t logB, uint64_t n,
                        uint32_t* nodes, uint64_t L, const MerkleTail* tail = nullptr);
