@@ -87,8 +87,8 @@ def valu_side(kernel: str, air: str, mode: str):
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--log-n", type=int, default=None, help="trace length 2^k (default: the config's)")
     ap.add_argument("--mode", choices=["replicas", "sharded"], default="replicas")
     ap.add_argument("--blowup", type=int, default=8)
