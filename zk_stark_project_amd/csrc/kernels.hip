@@ -569,6 +569,60 @@ __device__ __forceinline__ void merkle_leaf(const MerkleArgs& a, uint64_t i, uin
   }
 }
 
+// Quad-cooperative 2-to-1 merge for the narrow (latency-bound) tree levels: the
+// 4 lanes of a quad compute one BLAKE3(l || r) together, lane q holding state
+// column q (v[q], v[4+q], v[8+q], v[12+q]). A round is the column G on every
+// lane, a DPP quad rotation of rows b, c, d by 1, 2, 3 (the diagonals become
+// columns), the diagonal G, and the inverse rotation: ~3x shorter dependency
+// chain than one lane doing all 8 G's. Lane q returns output words q and 4+q.
+template <int K>
+__device__ __forceinline__ uint32_t quad_rot(uint32_t x) {  // value of lane (q + K) & 3
+  constexpr int ctrl = K == 1 ? 0x39 : (K == 2 ? 0x4E : 0x93);  // quad_perm [1,2,3,0] / [2,3,0,1] / [3,0,1,2]
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, ctrl, 0xF, 0xF, false);
+}
+__device__ __forceinline__ uint32_t sel4(uint32_t q, uint32_t x0, uint32_t x1, uint32_t x2, uint32_t x3) {
+  const uint32_t lo = (q & 1) ? x1 : x0, hi = (q & 1) ? x3 : x2;
+  return (q & 2) ? hi : lo;
+}
+__device__ __forceinline__ void merge_quad(const uint32_t m[16], uint32_t q, uint32_t& o0, uint32_t& o1) {
+  constexpr uint8_t S[7][16] = {{0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15},
+                                {2, 6, 3, 10, 7, 0, 4, 13, 1, 11, 12, 5, 9, 14, 15, 8},
+                                {3, 4, 10, 12, 13, 2, 7, 14, 6, 5, 9, 0, 11, 15, 8, 1},
+                                {10, 7, 12, 9, 14, 3, 13, 15, 4, 0, 11, 2, 5, 8, 1, 6},
+                                {12, 13, 9, 11, 15, 10, 14, 8, 7, 2, 5, 3, 0, 1, 6, 4},
+                                {9, 14, 11, 5, 8, 12, 15, 1, 13, 3, 0, 10, 2, 6, 4, 7},
+                                {11, 15, 5, 0, 1, 9, 8, 6, 14, 10, 2, 12, 3, 4, 7, 13}};
+  uint32_t a = sel4(q, b3::iv(0), b3::iv(1), b3::iv(2), b3::iv(3));
+  uint32_t b = sel4(q, b3::iv(4), b3::iv(5), b3::iv(6), b3::iv(7));
+  uint32_t c = a;                                    // v[8..12) = IV[0..4)
+  uint32_t d = sel4(q, 0u, 0u, 64u, b3::CHUNK_START | b3::CHUNK_END | b3::ROOT);  // counter, block_len, flags
+#define B3Q_G(x, y)                 \
+  a = a + b + (x);                  \
+  d = b3::rotr(d ^ a, 16);          \
+  c = c + d;                        \
+  b = b3::rotr(b ^ c, 12);          \
+  a = a + b + (y);                  \
+  d = b3::rotr(d ^ a, 8);           \
+  c = c + d;                        \
+  b = b3::rotr(b ^ c, 7);
+#pragma unroll
+  for (int r = 0; r < 7; r++) {
+    B3Q_G(sel4(q, m[S[r][0]], m[S[r][2]], m[S[r][4]], m[S[r][6]]),
+          sel4(q, m[S[r][1]], m[S[r][3]], m[S[r][5]], m[S[r][7]]))
+    b = quad_rot<1>(b);
+    c = quad_rot<2>(c);
+    d = quad_rot<3>(d);
+    B3Q_G(sel4(q, m[S[r][8]], m[S[r][10]], m[S[r][12]], m[S[r][14]]),
+          sel4(q, m[S[r][9]], m[S[r][11]], m[S[r][13]], m[S[r][15]]))
+    b = quad_rot<3>(b);
+    c = quad_rot<2>(c);
+    d = quad_rot<1>(d);
+  }
+#undef B3Q_G
+  o0 = a ^ c;
+  o1 = b ^ d;
+}
+
 __device__ __forceinline__ void merge8(const uint32_t l[8], const uint32_t r[8], uint32_t out[8]) {
   uint32_t m[16];
 #pragma unroll
@@ -603,6 +657,27 @@ __global__ __launch_bounds__(256) void k_merkle_fused(MerkleArgs a) {
   uint64_t lvl = L >> 1, lbase = base >> 1;
   for (uint32_t s = (uint32_t)(cnt >> 2); s >= 1; s >>= 1) {
     __syncthreads();
+    if (s <= 64) {  // narrow level: one quad per node
+      const uint32_t nd = t >> 2, q = t & 3;
+      uint32_t o0 = 0, o1 = 0;
+      if (t < 4 * s) {
+        uint32_t mm[16];
+#pragma unroll
+        for (int i = 0; i < 8; i++) { mm[i] = sd[(2 * nd) * 9 + i]; mm[8 + i] = sd[(2 * nd + 1) * 9 + i]; }
+        merge_quad(mm, q, o0, o1);
+      }
+      lvl >>= 1;
+      lbase >>= 1;
+      __syncthreads();
+      if (t < 4 * s) {
+        sd[nd * 9 + q] = o0;
+        sd[nd * 9 + 4 + q] = o1;
+        uint32_t* dst = a.nodes + (lvl + lbase + nd) * 8;
+        dst[q] = o0;
+        dst[4 + q] = o1;
+      }
+      continue;
+    }
     uint32_t o[8];
     if (t < s) {
       uint32_t l[8], r[8];
@@ -643,6 +718,25 @@ __global__ __launch_bounds__(256) void k_merkle_fused(MerkleArgs a) {
     }
     for (uint32_t sl = G / 4; sl >= 1; sl >>= 1) {
       __syncthreads();
+      if (sl <= 64) {  // narrow level: one quad per node
+        const uint32_t nd = t >> 2, q = t & 3;
+        uint32_t o0 = 0, o1 = 0;
+        if (t < 4 * sl) {
+          uint32_t mm[16];
+#pragma unroll
+          for (int k = 0; k < 8; k++) { mm[k] = sd[(2 * nd) * 9 + k]; mm[8 + k] = sd[(2 * nd + 1) * 9 + k]; }
+          merge_quad(mm, q, o0, o1);
+        }
+        __syncthreads();
+        if (t < 4 * sl) {
+          sd[nd * 9 + q] = o0;
+          sd[nd * 9 + 4 + q] = o1;
+          uint32_t* dst = a.nodes + (uint64_t)(sl + nd) * 8;
+          dst[q] = o0;
+          dst[4 + q] = o1;
+        }
+        continue;
+      }
       uint32_t o[8];
       if (t < sl) {
         uint32_t l[8], r[8];
