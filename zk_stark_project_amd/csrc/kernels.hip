@@ -707,14 +707,30 @@ __global__ __launch_bounds__(256) void k_merkle_fused(MerkleArgs a) {
   __threadfence();
   const uint32_t G = gridDim.x;
   if (G > 1) {
-    for (uint32_t i = t; i < G / 2; i += 256) {  // level G/2 from the roots in global memory
-      uint32_t l[8], r[8], o[8];
-      load_digest(a.nodes + (uint64_t)(G + 2 * i) * 8, l);
-      load_digest(a.nodes + (uint64_t)(G + 2 * i + 1) * 8, r);
-      merge8(l, r, o);
-      store_digest(a.nodes + (uint64_t)(G / 2 + i) * 8, o);
+    if (G / 2 <= 64) {  // level G/2 from the roots in global memory, one quad per node
+      const uint32_t nd = t >> 2, q = t & 3;
+      if (t < 4 * (G / 2)) {
+        uint32_t mm[16], o0, o1;
+        const uint32_t* src = a.nodes + (uint64_t)(G + 2 * nd) * 8;  // the node's two children, adjacent
 #pragma unroll
-      for (int k = 0; k < 8; k++) sd[i * 9 + k] = o[k];
+        for (int k = 0; k < 16; k++) mm[k] = src[k];
+        merge_quad(mm, q, o0, o1);
+        sd[nd * 9 + q] = o0;
+        sd[nd * 9 + 4 + q] = o1;
+        uint32_t* dst = a.nodes + (uint64_t)(G / 2 + nd) * 8;
+        dst[q] = o0;
+        dst[4 + q] = o1;
+      }
+    } else {
+      for (uint32_t i = t; i < G / 2; i += 256) {  // level G/2 from the roots in global memory
+        uint32_t l[8], r[8], o[8];
+        load_digest(a.nodes + (uint64_t)(G + 2 * i) * 8, l);
+        load_digest(a.nodes + (uint64_t)(G + 2 * i + 1) * 8, r);
+        merge8(l, r, o);
+        store_digest(a.nodes + (uint64_t)(G / 2 + i) * 8, o);
+#pragma unroll
+        for (int k = 0; k < 8; k++) sd[i * 9 + k] = o[k];
+      }
     }
     for (uint32_t sl = G / 4; sl >= 1; sl >>= 1) {
       __syncthreads();
