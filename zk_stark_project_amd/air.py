@@ -1,6 +1,6 @@
 """AIR descriptions mirrored from the reference (public inputs + metadata).
 
-The constraint arithmetic itself runs on the GPU (csrc/stark_kernels.hip);
+The constraint arithmetic itself runs on the GPU (csrc/kernels.hip);
 these classes carry what `Air::new` / `get_assertions` / `to_elements` carry
 in the reference so callers build identical public inputs.
 """
