@@ -104,3 +104,39 @@ def test_training_update_sharded_equals_single(ctx, rank_ctxs, world):
     ref, _ = ctx.prove(AIR_TRAINING_UPDATE, tr.data, pub, opts)
     res = prove_local_group(world, AIR_TRAINING_UPDATE, tr.data, pub, opts, contexts=rank_ctxs[:world])
     check_all_equal(res, ref)
+
+
+# ---------------------------------------------------------------- BASELINE configs[3] / configs[4]
+@pytest.mark.slow
+def test_mimc_c4_sharded(ctx, rank_ctxs):
+    """C4 (BASELINE configs[3]): MiMC 2^22, blowup 8, grinding 21, one proof split over
+    8 ranks by LDE coset. Every rank's bytes == the single-GPU proof == the oracle's."""
+    n = 1 << 22
+    opts = ProofOptions(40, 8, 21)
+    p, trace = mimc_case(n, opts)
+    pub = p.get_pub_inputs(trace).to_elements()
+    single, _ = ctx.prove(AIR_MIMC, trace.data, pub, opts)
+    res = prove_local_group(8, AIR_MIMC, trace.data, pub, opts, contexts=rank_ctxs[:8])
+    check_all_equal(res, single)
+    ref, _ = O.prove(AIR_MIMC, trace.to_bytes(), 1, n, to_bytes(pub), opts)
+    assert single == ref, "C4 single-GPU proof differs from the oracle"
+    assert O.verify(AIR_MIMC, single, to_bytes(pub), opts) == 0
+    _native.verify(AIR_MIMC, single, pub, opts)
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("world", [2, 8])
+def test_global_update_c5_sharded(ctx, rank_ctxs, world):
+    """C5 (BASELINE configs[4]): GlobalUpdate, 256 updates, 2^20 x 120 trace, reference
+    options (40, 16, 21), split over `world` ranks: every rank returns the single-GPU
+    proof bytes, which both verifiers accept. (The oracle would need ~40 s and 32 GiB
+    of host memory at this size: C3 carries the oracle comparison for this AIR.)"""
+    opts = ProofOptions.reference()
+    p = gu_prover(256, 1 << 20, opts, seed=5)
+    trace = p.build_trace()
+    pub = p.get_pub_inputs(trace).to_elements()
+    single, _ = ctx.prove(AIR_GLOBAL_UPDATE, trace.data, pub, opts)
+    res = prove_local_group(world, AIR_GLOBAL_UPDATE, trace.data, pub, opts, contexts=rank_ctxs[:world])
+    check_all_equal(res, single)
+    assert O.verify(AIR_GLOBAL_UPDATE, single, to_bytes(pub), opts) == 0
+    _native.verify(AIR_GLOBAL_UPDATE, single, pub, opts)
