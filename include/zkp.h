@@ -184,6 +184,55 @@ int zkp_merkle_commit_rows(zkp_ctx* ctx, const zkp_felt* cols, uint32_t width, u
  * smallest nonce >= 1 with trailing_zeros(u64_le(BLAKE3(seed || nonce_le)[0..8])) >= bits. */
 int zkp_grind(zkp_ctx* ctx, const uint8_t seed[32], uint32_t bits, uint64_t* nonce);
 
+/* ---- stage sessions: the plug-in hooks of a winter-prover fork ----------
+ * A zkp_session holds one proof's device-resident state (trace polynomials and
+ * LDE, composition evaluations and LDE, DEEP and FRI layers, Merkle trees), so
+ * a fork of winter-prover 0.12 keeps `Prover::prove` / `generate_proof` and its
+ * own channel (`DefaultRandomCoin<Blake3_256>`) and replaces only the stages:
+ *   zkp_session_trace_lde  ≙ Prover::new_trace_lde -> DefaultTraceLde::new
+ *                            (src/aggregation/prover.rs:216-224, src/training/prover.rs:273-281)
+ *   zkp_eval_constraints   ≙ Prover::new_evaluator(..).evaluate(..)
+ *                            (src/aggregation/prover.rs:226-233, src/training/prover.rs:283-290)
+ *   zkp_composition_commit ≙ Prover::build_constraint_commitment
+ *                            (src/aggregation/prover.rs:235-248, src/training/prover.rs:292-300)
+ *   zkp_ood_frame          ≙ the OOD frame of generate_proof (trace at z, z*g; composition at z)
+ *   zkp_deep_fri           ≙ DeepCompositionPoly + its LDE + FriProver::build_layers / set_remainder
+ *   zkp_query              ≙ trace_lde.query, constraint_commitment.query, fri_prover.build_proof
+ * (the last three are internal to winterfell 0.12's generate_proof).
+ * Calls must come in that order (ZKP_ERR_ARGUMENT otherwise); zkp_query may be
+ * repeated. Every value is bit-identical to the matching part of zkp_prove's proof
+ * when the caller's channel draws what zkp_prove's transcript draws. One GPU. */
+typedef struct zkp_session zkp_session;
+int zkp_session_create(zkp_ctx* ctx, zkp_air_id air, uint32_t width, uint64_t n, const zkp_felt* pub_elems,
+                       uint64_t n_pub, const zkp_proof_options* opts, zkp_session** out);
+/* Releases the session's device buffers (the ctx stays usable). */
+void zkp_session_destroy(zkp_session* s);
+/* Host trace (column-major width*n) -> interpolation, coset LDE, row commitment; root out. */
+int zkp_session_trace_lde(zkp_session* s, const zkp_felt* trace_cols, uint8_t root[32]);
+/* Composition coefficients as the caller's channel drew them (ConstraintCompositionCoefficients:
+ * the num_transition transition coefficients, then one per assertion) -> composition
+ * evaluations over the CE domain g*<w_{n*ce}> (stay in HBM for zkp_composition_commit;
+ * evals_out, nullable, receives the n*ce values in natural domain order). */
+int zkp_eval_constraints(zkp_session* s, const zkp_felt* coeffs, uint32_t n_coeffs, zkp_felt* evals_out);
+/* CompositionPoly::new (segments into C columns of n coefficients) + LDE + row commitment.
+ * evals = NULL: the session's zkp_eval_constraints output; otherwise n*ce host values in
+ * natural CE-domain order (e.g. from a CPU evaluator). num_columns (nullable) = C. */
+int zkp_composition_commit(zkp_session* s, const zkp_felt* evals, uint8_t root[32], uint32_t* num_columns);
+/* OOD frame at z: trace_ood[0..w) = T(z), trace_ood[w..2w) = T(z*w_n); comp_ood[0..C) = H_j(z). */
+int zkp_ood_frame(zkp_session* s, zkp_felt z, zkp_felt* trace_ood, zkp_felt* comp_ood);
+/* Called once per FRI layer with its Merkle root; returns that layer's alpha in *alpha
+ * (a fork binds it to `channel.commit_fri_layer(root); channel.draw_fri_alpha()`); non-zero aborts. */
+typedef int (*zkp_fri_channel)(void* user, uint32_t layer, const uint8_t root[32], zkp_felt* alpha);
+/* DEEP composition with the caller's coefficients (width + C), then the FRI layers (fold 16)
+ * and the remainder polynomial: remainder (nullable; capacity *remainder_len) receives its
+ * coefficients, *remainder_len their count, remainder_commitment = hash_elements(remainder). */
+int zkp_deep_fri(zkp_session* s, const zkp_felt* deep_coeffs, zkp_fri_channel channel, void* user,
+                 zkp_felt* remainder, uint64_t* remainder_len, uint8_t remainder_commitment[32]);
+/* Openings at sorted, unique LDE positions (< n*blowup): returns, in zkp_prove's wire
+ * format, u8(1) | trace values | trace batch paths | constraint values | constraint batch
+ * paths | u8(L) | per FRI layer: values | batch paths. Free with zkp_free. */
+int zkp_query(zkp_session* s, const uint64_t* positions, uint64_t n_positions, uint8_t** out, uint64_t* out_len);
+
 /* ---- verification (≙ winterfell `verify`) ------------------------------ */
 /* Status codes of zkp_verify; values map onto winter-verifier `VerifierError`. */
 typedef enum zkp_verify_status {

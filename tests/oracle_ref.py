@@ -160,3 +160,42 @@ def grind(seed: bytes, bits: int) -> int:
 def felts_from_bytes(b: bytes):
     a = np.frombuffer(b, dtype="<u8").reshape(-1, 2)
     return [int(lo) | (int(hi) << 64) for lo, hi in a]
+
+
+class Stages(ctypes.Structure):
+    """oracle_stages (oracle/stark_oracle.c): stage values of one oracle proof."""
+    _fields_ = [("coeffs", ctypes.c_void_p), ("comp_evals", ctypes.c_void_p), ("ood", ctypes.c_void_p),
+                ("deep_coeffs", ctypes.c_void_p), ("alphas", ctypes.c_void_p), ("remainder", ctypes.c_void_p),
+                ("n_coeffs", ctypes.c_uint32), ("n_layers", ctypes.c_uint32), ("n_remainder", ctypes.c_uint32),
+                ("pad", ctypes.c_uint32)]
+
+
+def prove_stages(air_id: int, trace_cols: bytes, width: int, n: int, pub: bytes, opts, ce: int, C: int):
+    """Oracle proof + its stage values: dict of byte strings (16 B LE felts) keyed
+    coeffs, comp_evals (n*ce, natural CE order), ood (2w + C), deep_coeffs (w + C),
+    alphas (one per FRI layer), remainder."""
+    L = lib()
+    L.oracle_prove_stages.restype = ctypes.c_int
+    L.oracle_prove_stages.argtypes = [ctypes.c_int, ctypes.c_char_p, ctypes.c_uint32, ctypes.c_uint64,
+                                      ctypes.c_char_p, ctypes.c_uint64, ctypes.POINTER(ProofOptionsC),
+                                      ctypes.POINTER(ctypes.POINTER(ctypes.c_uint8)),
+                                      ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(Stages)]
+    bufs = {"coeffs": ctypes.create_string_buffer(16 * 1024), "comp_evals": ctypes.create_string_buffer(16 * n * ce),
+            "ood": ctypes.create_string_buffer(16 * (2 * width + C)),
+            "deep_coeffs": ctypes.create_string_buffer(16 * (width + C)),
+            "alphas": ctypes.create_string_buffer(16 * 16), "remainder": ctypes.create_string_buffer(16 * 256)}
+    sd = Stages(*[ctypes.cast(bufs[k], ctypes.c_void_p) for k in
+                  ("coeffs", "comp_evals", "ood", "deep_coeffs", "alphas", "remainder")], 0, 0, 0, 0)
+    out = ctypes.POINTER(ctypes.c_uint8)()
+    olen = ctypes.c_uint64()
+    oc = opts_c(opts)
+    rc = L.oracle_prove_stages(air_id, trace_cols, width, n, pub, len(pub) // 16, ctypes.byref(oc),
+                               ctypes.byref(out), ctypes.byref(olen), ctypes.byref(sd))
+    if rc != 0:
+        raise RuntimeError(f"oracle_prove_stages failed: {rc}")
+    proof = ctypes.string_at(out, olen.value)
+    L.oracle_free(out)
+    res = {"coeffs": bufs["coeffs"].raw[:16 * sd.n_coeffs], "comp_evals": bufs["comp_evals"].raw,
+           "ood": bufs["ood"].raw, "deep_coeffs": bufs["deep_coeffs"].raw,
+           "alphas": bufs["alphas"].raw[:16 * sd.n_layers], "remainder": bufs["remainder"].raw[:16 * sd.n_remainder]}
+    return proof, res

@@ -72,7 +72,13 @@ EXPORTED = [
     "zkp_build_mimc_trace", "zkp_prove_sharded", "zkp_comm_local_group", "zkp_comm_rccl_unique_id",
     "zkp_comm_rccl_create", "zkp_comm_destroy", "zkp_comm_rank", "zkp_comm_world", "zkp_prove_sharded_device",
     "zkp_verify", "zkp_build_global_update_trace", "zkp_set_profiling_kernel",
+    "zkp_session_create", "zkp_session_destroy", "zkp_session_trace_lde", "zkp_eval_constraints",
+    "zkp_composition_commit", "zkp_ood_frame", "zkp_deep_fri", "zkp_query",
 ]
+
+# int (*zkp_fri_channel)(void* user, uint32_t layer, const uint8_t root[32], zkp_felt* alpha)
+FRI_CHANNEL = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint8),
+                               ctypes.c_void_p)
 
 # zkp_verify_status (include/zkp.h) -> winter-verifier `VerifierError` variant
 VERIFY_STATUS = {
@@ -147,6 +153,15 @@ def load():
         L.zkp_verify.argtypes = [i32, ctypes.c_char_p, u64, vp, u64, popt]
         L.zkp_verify.restype = i32
         L.zkp_build_global_update_trace.argtypes = [vp, vp, vp, vp, u64, Felt, u64, vp, vp]
+        L.zkp_session_create.argtypes = [vp, i32, u32, u64, vp, u64, popt, ctypes.POINTER(vp)]
+        L.zkp_session_destroy.argtypes = [vp]
+        L.zkp_session_destroy.restype = None
+        L.zkp_session_trace_lde.argtypes = [vp, vp, ctypes.c_char_p]
+        L.zkp_eval_constraints.argtypes = [vp, vp, u32, vp]
+        L.zkp_composition_commit.argtypes = [vp, vp, ctypes.c_char_p, ctypes.POINTER(u32)]
+        L.zkp_ood_frame.argtypes = [vp, Felt, vp, vp]
+        L.zkp_deep_fri.argtypes = [vp, vp, FRI_CHANNEL, vp, vp, ctypes.POINTER(u64), ctypes.c_char_p]
+        L.zkp_query.argtypes = [vp, ctypes.POINTER(u64), u64, ctypes.POINTER(pu8), ctypes.POINTER(u64)]
         _lib = L
         return L
 
@@ -394,3 +409,110 @@ class Context:
             name, cnt, ms, nbytes = line.split()
             out[name] = {"launches": int(cnt), "ms": float(ms), "bytes": float(nbytes)}
         return out
+
+
+def _felts(vals) -> np.ndarray:
+    return np.ascontiguousarray(np.array([[int(v) & (2**64 - 1), int(v) >> 64] for v in vals],
+                                         dtype=np.uint64).reshape(-1, 2))
+
+
+def _ints(a: np.ndarray) -> list:
+    return [int(lo) | (int(hi) << 64) for lo, hi in a.reshape(-1, 2)]
+
+
+class Session:
+    """One proof driven stage by stage (`zkp_session`, include/zkp.h): the plug-in
+    hooks a winter-prover fork calls from its own `generate_proof` with its own
+    channel. Stages: trace_lde -> eval_constraints -> composition_commit ->
+    ood_frame -> deep_fri -> query."""
+
+    def __init__(self, ctx: "Context", air_id: int, width: int, n: int, pub, options: ProofOptions):
+        self.ctx, self.lib, self.width, self.n = ctx, ctx.lib, width, n
+        self.ce = 8 if air_id == 1 else 2  # constraint-evaluation blowup: MiMC degree 7, linear AIRs degree 1
+        self.ptr = ctypes.c_void_p()
+        self._pub = _felts(pub) if len(pub) else None
+        self._opts = options.to_c()
+        ctx._check(self.lib.zkp_session_create(ctx.ptr, air_id, width, n,
+                                               self._pub.ctypes.data if self._pub is not None else None,
+                                               len(pub), ctypes.byref(self._opts), ctypes.byref(self.ptr)),
+                   "zkp_session_create")
+        self.num_columns = None
+
+    def close(self):
+        if self.ptr:
+            self.lib.zkp_session_destroy(self.ptr)
+            self.ptr = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def trace_lde(self, trace: np.ndarray) -> bytes:
+        """trace: (width, n, 2) uint64 column-major -> trace commitment root."""
+        trace = np.ascontiguousarray(trace, dtype=np.uint64)
+        root = ctypes.create_string_buffer(32)
+        self.ctx._check(self.lib.zkp_session_trace_lde(self.ptr, trace.ctypes.data, root), "zkp_session_trace_lde")
+        return root.raw
+
+    def eval_constraints(self, coeffs, want_evals: bool = True):
+        """composition coefficients -> n*ce evaluations (natural CE-domain order) or None."""
+        c = _felts(coeffs)
+        out = None
+        if want_evals:
+            out = np.zeros((self.n * self.ce, 2), dtype=np.uint64)
+        self.ctx._check(self.lib.zkp_eval_constraints(self.ptr, c.ctypes.data, len(coeffs),
+                                                      out.ctypes.data if out is not None else None),
+                        "zkp_eval_constraints")
+        return out
+
+    def composition_commit(self, evals: np.ndarray | None = None) -> bytes:
+        root = ctypes.create_string_buffer(32)
+        nc = ctypes.c_uint32()
+        e = np.ascontiguousarray(evals, dtype=np.uint64) if evals is not None else None
+        self.ctx._check(self.lib.zkp_composition_commit(self.ptr, e.ctypes.data if e is not None else None, root,
+                                                        ctypes.byref(nc)), "zkp_composition_commit")
+        self.num_columns = nc.value
+        return root.raw
+
+    def ood_frame(self, z: int):
+        """-> (trace_ood: 2*width ints [T(z) | T(zg)], comp_ood: C ints)."""
+        t = np.zeros((2 * self.width, 2), dtype=np.uint64)
+        c = np.zeros((self.num_columns, 2), dtype=np.uint64)
+        self.ctx._check(self.lib.zkp_ood_frame(self.ptr, Felt(z & (2**64 - 1), z >> 64), t.ctypes.data,
+                                               c.ctypes.data), "zkp_ood_frame")
+        return _ints(t), _ints(c)
+
+    def deep_fri(self, deep_coeffs, channel):
+        """channel(layer, root: bytes) -> alpha (int). Returns (remainder ints, remainder commitment)."""
+        g = _felts(deep_coeffs)
+        err = []
+
+        def cb(user, layer, root, alpha_p):
+            try:
+                a = int(channel(int(layer), bytes(root[:32])))
+                ctypes.cast(alpha_p, ctypes.POINTER(Felt))[0] = Felt(a & (2**64 - 1), a >> 64)
+                return 0
+            except Exception as e:  # noqa: BLE001 — re-raised after the call
+                err.append(e)
+                return 1
+        fn = FRI_CHANNEL(cb)
+        rem = np.zeros((256, 2), dtype=np.uint64)
+        rlen = ctypes.c_uint64(256)
+        commit = ctypes.create_string_buffer(32)
+        rc = self.lib.zkp_deep_fri(self.ptr, g.ctypes.data, fn, None, rem.ctypes.data, ctypes.byref(rlen), commit)
+        if err:
+            raise err[0]
+        self.ctx._check(rc, "zkp_deep_fri")
+        return _ints(rem[:rlen.value]), commit.raw
+
+    def query(self, positions) -> bytes:
+        pos = (ctypes.c_uint64 * len(positions))(*positions)
+        out = ctypes.POINTER(ctypes.c_uint8)()
+        olen = ctypes.c_uint64()
+        self.ctx._check(self.lib.zkp_query(self.ptr, pos, len(positions), ctypes.byref(out), ctypes.byref(olen)),
+                        "zkp_query")
+        data = ctypes.string_at(out, olen.value)
+        self.lib.zkp_free(out)
+        return data

@@ -14,6 +14,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <memory>
 #include <stdexcept>
 #include <string>
 #include <utility>
@@ -255,6 +256,22 @@ struct zkp_ctx {
         bufs["Si_" + std::to_string(logn) + "_" + std::to_string(logB) + "_" + std::to_string(logce)].p);
   }
 
+  // release the buffers whose names start with `prefix` (a stage session's state)
+  void drop(const std::string& prefix) {
+    sync();
+    for (auto it = bufs.begin(); it != bufs.end();) {
+      if (it->first.compare(0, prefix.size(), prefix) == 0) {
+        if (it->second.p) HIP_CHECK(hipFree(it->second.p));
+        it = bufs.erase(it);
+      } else {
+        ++it;
+      }
+    }
+    for (auto it = cached.begin(); it != cached.end();)
+      it = it->first.compare(0, prefix.size(), prefix) == 0 ? cached.erase(it) : std::next(it);
+  }
+  uint64_t next_session = 0;
+
   zkp_comm* self = nullptr;
   zkp_comm* self_comm() {
     if (!self) self = make_self_comm();
@@ -409,6 +426,334 @@ felt* ood_launch(zkp_ctx* ctx, const felt* arrays, uint32_t narrays, uint32_t nt
   return dv;
 }
 
+// Domain points of every LDE coset j (g*w_N^j, entries [0, B)) and CE coset u
+// (g*w_M^u, entries [B, B+ce)); domain-only, cached per (n, B, ce).
+felt* coset_points(zkp_ctx* ctx, uint32_t logn, uint32_t logB, uint32_t logce) {
+  const uint32_t B = 1u << logB, ce = 1u << logce;
+  const std::string cxkey = "coset_x_" + std::to_string(logn) + "_" + std::to_string(logB) + "_" +
+                            std::to_string(logce);
+  felt* cx = ctx->buf<felt>(cxkey, B + ce);
+  if (!ctx->have_cached(cxkey)) {
+    std::vector<felt> h(B + ce);
+    const felt g = felt_u64(3);
+    felt wN = root_of_unity(logn + logB), wM = root_of_unity(logn + logce);
+    for (uint32_t j = 0; j < B; j++) h[j] = mul(g, pow_u64(wN, j));
+    for (uint32_t u = 0; u < ce; u++) h[B + u] = mul(g, pow_u64(wM, u));
+    ctx->upload(cx, h.data(), h.size() * 16);
+  }
+  return cx;
+}
+
+// DefaultConstraintEvaluator::evaluate over the CE cosets [u0, u0 + cel) held by
+// this rank (its LDE cosets are [j0, j0 + 2^logBl)): composition evaluations
+// comp[ul * n + t] = H(g * w_M^(u0+ul) * w_n^t), i.e. CE domain index (u0+ul) + ce*t.
+// dt_cc = the composition coefficients (device; transition then boundary).
+void constraint_eval(zkp_ctx* ctx, const AirDesc& air, uint32_t logn, uint32_t logB, uint32_t logce, uint32_t u0,
+                     uint32_t cel, uint32_t j0, uint32_t logBl, const felt* cx, const felt* twn, const felt* dt_cc,
+                     const felt* dt_aval, const felt* tlde, felt* comp) {
+  Prof& pf = ctx->prof;
+  hipStream_t st = ctx->stream;
+  const uint32_t B = 1u << logB, ce = 1u << logce, logN = logn + logB, w = air.w;
+  const uint64_t n = 1ull << logn;
+  const felt g = felt_u64(3);
+  felt wn = root_of_unity(logn);
+  EvalCommon ec;
+  ec.logn = logn; ec.logB = logB; ec.logce = logce; ec.logN = logN;
+  ec.u0 = u0; ec.cel = cel; ec.j0 = j0; ec.logBl = logBl;
+  ec.g = g;
+  ec.w_last = pow_u64(wn, n - 1);
+  ec.pm = PointMap{cx + B + u0, twn, logn};
+  // 1/(x^n - 1) on the CE domain: x^n = g^n * w_ce^s (domain-only: cached per (n, ce))
+  const std::string zkey = "zinv_" + std::to_string(logn) + "_" + std::to_string(logce);
+  std::vector<felt>& zinv = ctx->host_cache[zkey];
+  if (zinv.empty()) {
+    zinv.resize(ce);
+    felt gn = pow_u64(g, n), wce = root_of_unity(logce);
+    for (uint32_t s = 0; s < ce; s++) zinv[s] = inv(sub(mul(gn, pow_u64(wce, s)), one()));
+  }
+  felt* dz = ctx->buf<felt>(zkey, ce);
+  if (!ctx->have_cached(zkey)) ctx->upload(dz, zinv.data(), ce * 16);
+  // coefficient-dependent constants, built on the device from the drawn coefficients
+  // (MiMC: Z_T constants with the transition coefficient folded in, then b0, b1;
+  // linear AIRs: the 4 coefficient rows + the two boundary sums)
+  const uint32_t lw = air.id == ZKP_AIR_TRAINING_UPDATE ? w / 2 : w;
+  felt* dconst = ctx->buf<felt>("eval_consts", air.id == ZKP_AIR_MIMC ? (size_t)ce + 2 : 4 * (size_t)lw + 2);
+  launch_dt_eval_consts(pf, st, air.id, dt_cc, air.k, dt_aval, dz, ce, w, air.num_t, dconst);
+  ec.zinv = air.id == ZKP_AIR_MIMC ? dconst : dz;
+  const std::string dom = std::to_string(logn) + "_" + std::to_string(logB) + "_" + std::to_string(u0) + "_" +
+                          std::to_string(cel);
+  if (air.id == ZKP_AIR_MIMC) {
+    // periodic column K over the CE domain: interpolate over <w_64>, evaluate at g^(n/64) * <w_{64 ce}>
+    // (domain-only: cached per (n, ce))
+    const std::string kkey = "kper_" + std::to_string(logn) + "_" + std::to_string(logce);
+    felt* dk = ctx->buf<felt>(kkey, 64 * (size_t)ce);
+    if (!ctx->have_cached(kkey)) {
+      std::vector<felt> kc(64);
+      for (int j = 0; j < 64; j++) kc[j] = felt_u64((uint64_t)(j + 1) * 1000000ull);
+      host_interpolate(kc, one());
+      std::vector<felt> kv = host_evaluate(kc, 64 * ce, pow_u64(g, n / 64));
+      ctx->upload(dk, kv.data(), kv.size() * 16);
+    }
+    MimcEvalArgs ma;
+    ma.bcoef = dconst + ce;  // b0, b1
+    ma.v0 = air.a_val[0];
+    ma.v1 = air.a_val[1];
+    ma.kper = dk;
+    // divisor inverses depend only on the domain and the assertion steps: cache per config
+    std::string key = "binv_mimc_" + dom;
+    ma.binv_ready = ctx->have_cached(key);
+    ma.binv = ctx->buf<felt>("binv_scratch", ((uint64_t)cel * n) / 2048 + 1);
+    ma.dinv = ctx->buf<felt>(key, (uint64_t)cel * n);
+    launch_eval_mimc(pf, st, ec, ma, tlde, comp);
+  } else if (air.id == ZKP_AIR_GLOBAL_UPDATE) {
+    // GlobalUpdate: T = sum_i a^i (k*next_i - k*cur_i - next_{i+60}); B = sum_c b_c (cur_c - v_c)
+    LinearEvalArgs la;
+    la.width = w;
+    la.transition = true;
+    la.two_groups = false;
+    la.coefs = dconst;  // [next | cur | beta0 | beta1 | bconst0, bconst1]
+    la.w_bstep = pow_u64(wn, air.a_step[0]);
+    la.w_bstep1 = zero();
+    std::string key = "binv_lin_" + dom + "_" + std::to_string(air.a_step[0]);
+    la.binv_ready = ctx->have_cached(key);
+    la.binv = ctx->buf<felt>("binv_scratch", ((uint64_t)cel * n) / 2048 + 1);
+    la.dinv = ctx->buf<felt>(key, (uint64_t)cel * n);
+    launch_eval_linear(pf, st, ec, la, tlde, comp);
+  } else {
+    // TrainingUpdate: transitions identically zero; boundary groups at rows 0 and n-1 over
+    // the masked columns 0..w/2 (the mask columns are never read)
+    const uint32_t half = w / 2;
+    LinearEvalArgs la;
+    la.width = half;
+    la.transition = false;
+    la.two_groups = true;
+    la.coefs = dconst;
+    la.w_bstep = one();
+    la.w_bstep1 = ec.w_last;
+    std::string key = "binv_tu_" + dom;
+    la.binv_ready = ctx->have_cached(key);
+    la.binv = ctx->buf<felt>("binv_scratch", ((uint64_t)cel * n) / 2048 + 1);
+    la.dinv = ctx->buf<felt>(key, (uint64_t)cel * n);
+    launch_eval_linear(pf, st, ec, la, tlde, comp);
+  }
+}
+
+// one FRI layer as the prover holds it: coset-major evaluations of the cosets
+// [jc, jc + Bc) (m positions each), and its (possibly sharded) Merkle tree
+struct FriLayer {
+  felt* E = nullptr;
+  uint64_t m = 0;
+  uint32_t Bc = 0, jc = 0;
+  bool sharded = false;
+  TreeShard tree;
+};
+
+// Query openings of one proof: trace and constraint rows + their batch Merkle
+// paths, FRI layer rows + paths, gathered from device memory (from the owning
+// rank when sharded) and written in the proof's wire format (Queries /
+// FriProof of winterfell's Proof::to_bytes).
+struct Openings {
+  std::vector<uint32_t> gathered;
+  std::vector<GatherSeg> segs;
+  BatchPlan bt;               // trace and constraint trees (same shape and positions)
+  std::vector<BatchPlan> bf;  // FRI layer trees
+  size_t cursor = 0;
+  // values and batch paths are written straight from the gathered words
+  // (felts are stored canonical LE, i.e. already in their wire format)
+  void write_values(Writer& wr) {
+    const GatherSeg& gs = segs[cursor++];
+    wr.u32((uint32_t)(gs.count * 16));
+    wr.put(gathered.data() + gs.out_off, gs.count * 16);
+  }
+  void write_batch(Writer& wr, const BatchPlan& bp) {
+    const GatherSeg& gs = segs[cursor++];
+    const uint32_t* d = gathered.data() + gs.out_off;
+    size_t nodes = 0;
+    for (auto& p : bp.paths) nodes += p.size();
+    wr.u32((uint32_t)(2 + bp.paths.size() + 32 * nodes));
+    wr.u8((uint8_t)bp.depth);
+    wr.u8((uint8_t)bp.paths.size());
+    size_t k = 0;
+    for (auto& p : bp.paths) {
+      wr.u8((uint8_t)p.size());
+      wr.put(d + 8 * k, 32 * p.size());
+      k += p.size();
+    }
+  }
+  // trace + constraint queries: values and batch paths of each commitment
+  void write_commitment_queries(Writer& wr) {
+    cursor = 0;
+    for (int seg = 0; seg < 2; seg++) {
+      write_values(wr);
+      write_batch(wr, bt);
+    }
+  }
+  // FRI proof layers (values + batch paths per layer), after the commitment queries
+  void write_fri_queries(Writer& wr) {
+    cursor = 4;
+    for (const BatchPlan& b : bf) {
+      write_values(wr);
+      write_batch(wr, b);
+    }
+  }
+};
+
+// Gathers every opening at the sorted unique LDE positions `pos` (this rank
+// holds the LDE cosets [j0, j0 + Bl)); collective over cm when sharded.
+void gather_openings(zkp_ctx* ctx, zkp_comm* cm, const std::vector<uint64_t>& pos, uint64_t n, uint32_t logB,
+                     uint32_t j0, const felt* tlde, uint32_t w, const TreeShard& ttree, const felt* clde, uint32_t C,
+                     const TreeShard& ctree, const std::vector<FriLayer>& layers, uint32_t L, uint32_t F,
+                     Openings& op) {
+  Prof& pf = ctx->prof;
+  hipStream_t st = ctx->stream;
+  const uint32_t R = (uint32_t)cm->world, rank = (uint32_t)cm->rank;
+  const uint32_t B = 1u << logB, Bl = B / R;
+  const uint64_t N = n << logB;
+  // Openings: every item is (owner rank, local index) or a host-side top node.
+  // Each rank gathers all items from its own memory (index 0 for items it does
+  // not own), the gathered buffers are all-gathered, and every item is taken
+  // from its owner's copy.
+  struct SegPlan {
+    const void* src;
+    std::vector<uint64_t> idx;
+    std::vector<int32_t> owner;  // -1: host top node (value in host_dig)
+    std::vector<const uint8_t*> host_dig;
+    uint32_t words;
+  };
+  auto row_owner = [&](uint64_t j) -> uint32_t { return R > 1 ? (uint32_t)(j / Bl) : 0; };
+  auto lde_values = [&](const felt* src, uint32_t cols) {
+    SegPlan sp{src, {}, {}, {}, 4};
+    sp.idx.reserve(pos.size() * cols);
+    sp.owner.reserve(pos.size() * cols);
+    sp.host_dig.reserve(pos.size() * cols);
+    for (uint64_t p : pos) {
+      uint64_t j = p & (B - 1), t = p >> logB;
+      uint32_t ow = row_owner(j);
+      for (uint32_t c = 0; c < cols; c++) {
+        sp.idx.push_back(ow == rank ? ((uint64_t)c * Bl + (j - j0)) * n + t : 0);
+        sp.owner.push_back((int32_t)ow);
+        sp.host_dig.push_back(nullptr);
+      }
+    }
+    return sp;
+  };
+  auto path_nodes = [&](const TreeShard& tr, const BatchPlan& bp) {
+    SegPlan sp{tr.nodes, {}, {}, {}, 8};
+    for (auto& pth : bp.paths)
+      for (uint64_t k : pth) {
+        TreeShard::Loc lc = tr.locate(k);
+        if (lc.host) {
+          sp.idx.push_back(0);
+          sp.owner.push_back(-1);
+          sp.host_dig.push_back(tr.top[lc.local].data());
+        } else {
+          sp.idx.push_back(lc.owner == (tr.logR ? rank : 0u) ? lc.local : 0);
+          sp.owner.push_back(tr.logR ? (int32_t)lc.owner : (int32_t)rank);
+          sp.host_dig.push_back(nullptr);
+        }
+      }
+    return sp;
+  };
+  op.bt = plan_batch(N, pos);
+  const BatchPlan& bt = op.bt;
+  const BatchPlan& bc = bt;  // the constraint tree has the same shape and positions
+  std::vector<std::vector<uint64_t>> fpos(L);
+  op.bf.assign(L, BatchPlan{});
+  std::vector<BatchPlan>& bf = op.bf;
+  std::vector<SegPlan> plan;
+  plan.push_back(lde_values(tlde, w));
+  plan.push_back(path_nodes(ttree, bt));
+  plan.push_back(lde_values(clde, C));
+  plan.push_back(path_nodes(ctree, bc));
+  {
+    std::vector<uint64_t> cur = pos;
+    for (uint32_t l = 0; l < L; l++) {
+      const FriLayer& ly = layers[l];
+      const uint64_t m16 = ly.m / F, Rows = (uint64_t)B * m16;
+      fpos[l] = fold_positions(cur, Rows);
+      bf[l] = plan_batch(Rows, fpos[l]);
+      SegPlan sp{ly.E, {}, {}, {}, 4};
+      for (uint64_t r : fpos[l])
+        for (uint32_t k = 0; k < F; k++) {
+          uint64_t i = r + k * Rows;  // natural index in the layer
+          uint64_t j = i & (B - 1), tt = i >> logB;
+          uint32_t ow = ly.sharded ? (uint32_t)(j / Bl) : rank;
+          sp.idx.push_back(ow == rank ? (j - ly.jc) * ly.m + tt : 0);
+          sp.owner.push_back((int32_t)ow);
+          sp.host_dig.push_back(nullptr);
+        }
+      plan.push_back(sp);
+      plan.push_back(path_nodes(ly.tree, bf[l]));
+      cur = fpos[l];
+    }
+  }
+  std::vector<GatherSeg>& segs = op.segs;
+  segs.clear();
+  std::vector<uint64_t> all_idx;
+  uint64_t out_words = 0, max_count = 1;
+  for (auto& sp : plan) {
+    GatherSeg gs;
+    gs.src = sp.src;
+    gs.idx_off = all_idx.size();
+    gs.count = sp.idx.size();
+    gs.out_off = out_words;
+    gs.words = sp.words;
+    gs.pad = 0;
+    all_idx.insert(all_idx.end(), sp.idx.begin(), sp.idx.end());
+    out_words += gs.count * sp.words;
+    max_count = std::max<uint64_t>(max_count, gs.count);
+    segs.push_back(gs);
+  }
+  size_t seg_bytes = segs.size() * sizeof(GatherSeg), idx_bytes = all_idx.size() * 8;
+  size_t up_bytes = seg_bytes + idx_bytes, down_bytes = out_words * 4;
+  ctx->stage_end("7a_query_plan");
+  uint8_t* hp = (uint8_t*)ctx->pinned(std::max(up_bytes, down_bytes * R) + 64);
+  memcpy(hp, segs.data(), seg_bytes);
+  memcpy(hp + seg_bytes, all_idx.data(), idx_bytes);
+  uint8_t* dup = ctx->buf<uint8_t>("gather_in", up_bytes + 16);
+  uint32_t* dout = ctx->buf<uint32_t>("gather_out", out_words + 4);
+  uint32_t* dall = R > 1 ? ctx->buf<uint32_t>("gather_all", out_words * R + 4) : dout;
+  HIP_CHECK(hipMemcpyAsync(dup, hp, up_bytes, hipMemcpyHostToDevice, st));
+  launch_gather_multi(pf, st, (const GatherSeg*)dup, (uint32_t)segs.size(), max_count,
+                      (const uint64_t*)(dup + seg_bytes), dout, (double)down_bytes * 2);
+  if (R > 1) cm->all_gather(st, dout, dall, down_bytes);
+  HIP_CHECK(hipMemcpyAsync(hp, dall, down_bytes * R, hipMemcpyDeviceToHost, st));
+  ctx->sync();
+  ctx->stage_end("7b_gather");
+  op.gathered.assign(out_words, 0);
+  std::vector<uint32_t>& gathered = op.gathered;
+  {
+    const uint32_t* all = reinterpret_cast<const uint32_t*>(hp);
+    for (size_t si = 0; si < plan.size(); si++) {
+      const SegPlan& sp = plan[si];
+      const GatherSeg& gs = segs[si];
+      for (size_t it = 0; it < sp.idx.size(); it++) {
+        uint32_t* dst = gathered.data() + gs.out_off + it * sp.words;
+        if (sp.owner[it] < 0) {
+          memcpy(dst, sp.host_dig[it], 32);
+        } else {
+          uint32_t ow = R > 1 ? (uint32_t)sp.owner[it] : 0;
+          memcpy(dst, all + (size_t)ow * out_words + gs.out_off + it * sp.words, sp.words * 4);
+        }
+      }
+    }
+  }
+}
+
+// constants of the fold-16 iDFT (w_16^-m for m < 8, then 16^-1), cached per context
+const felt* fold_constants(zkp_ctx* ctx) {
+  felt* deps = ctx->buf<felt>("eps_inv", 9);
+  if (!ctx->have_cached("eps_inv")) {
+    std::vector<felt> eps(9);
+    felt einv = inv(root_of_unity(4));
+    eps[0] = one();
+    for (int m = 1; m < 8; m++) eps[m] = mul(eps[m - 1], einv);
+    eps[8] = inv(felt_u64(16));
+    ctx->upload(deps, eps.data(), 9 * 16);
+  }
+  return deps;
+}
+
 int prove_impl(zkp_ctx* ctx, zkp_comm* cm, int air_id, const felt* d_trace, uint32_t w, uint64_t n,
                const zkp_felt* pub_elems, uint64_t n_pub, const zkp_proof_options* o, uint8_t** proof,
                uint64_t* proof_len, zkp_transcript* tr_out) {
@@ -480,16 +825,7 @@ int prove_impl(zkp_ctx* ctx, zkp_comm* cm, int air_id, const felt* d_trace, uint
   const felt* Sj0 = ctx->S(logn, logB) + (uint64_t)j0 * n;
   // domain points: coset offsets g*w_N^j (LDE cosets) and g*w_M^u (CE cosets), w_n^t table
   // (domain-only: cached per (n, B, ce), so no upload sits between the proof's kernels)
-  const std::string cxkey = "coset_x_" + std::to_string(logn) + "_" + std::to_string(logB) + "_" +
-                            std::to_string(logce);
-  felt* cx = ctx->buf<felt>(cxkey, B + ce);
-  if (!ctx->have_cached(cxkey)) {
-    std::vector<felt> h(B + ce);
-    felt wN = root_of_unity(logN), wM = root_of_unity(logn + logce);
-    for (uint32_t j = 0; j < B; j++) h[j] = mul(g, pow_u64(wN, j));
-    for (uint32_t u = 0; u < ce; u++) h[B + u] = mul(g, pow_u64(wM, u));
-    ctx->upload(cx, h.data(), h.size() * 16);
-  }
+  felt* cx = coset_points(ctx, logn, logB, logce);
   const felt* twn = ctx->tws(logN) + ((1ull << (logn - 1)) - 1);
   ctx->stage_end("0_setup");
 
@@ -525,88 +861,7 @@ int prove_impl(zkp_ctx* ctx, zkp_comm* cm, int air_id, const felt* d_trace, uint
   // 3. constraint composition coefficients (drawn on the device) + evaluation (DefaultConstraintEvaluator)
   if (!coeffs_drawn) launch_dt_draw_coeffs(pf, st, dt_seed, troot_d, o->batching_constraints, ncoef, dt_cc);
   felt* comp = ctx->buf<felt>("comp", (size_t)(cel ? cel : 1) * n);
-  if (cel) {
-    felt wn = root_of_unity(logn);
-    EvalCommon ec;
-    ec.logn = logn; ec.logB = logB; ec.logce = logce; ec.logN = logN;
-    ec.u0 = u0; ec.cel = cel; ec.j0 = j0; ec.logBl = logBl;
-    ec.g = g;
-    ec.w_last = pow_u64(wn, n - 1);
-    ec.pm = PointMap{cx + B + u0, twn, logn};
-    // 1/(x^n - 1) on the CE domain: x^n = g^n * w_ce^s (domain-only: cached per (n, ce))
-    const std::string zkey = "zinv_" + std::to_string(logn) + "_" + std::to_string(logce);
-    std::vector<felt>& zinv = ctx->host_cache[zkey];
-    if (zinv.empty()) {
-      zinv.resize(ce);
-      felt gn = pow_u64(g, n), wce = root_of_unity(logce);
-      for (uint32_t s = 0; s < ce; s++) zinv[s] = inv(sub(mul(gn, pow_u64(wce, s)), one()));
-    }
-    felt* dz = ctx->buf<felt>(zkey, ce);
-    if (!ctx->have_cached(zkey)) ctx->upload(dz, zinv.data(), ce * 16);
-    // coefficient-dependent constants, built on the device from the drawn coefficients
-    // (MiMC: Z_T constants with the transition coefficient folded in, then b0, b1;
-    // linear AIRs: the 4 coefficient rows + the two boundary sums)
-    const uint32_t lw = air.id == ZKP_AIR_TRAINING_UPDATE ? w / 2 : w;
-    felt* dconst = ctx->buf<felt>("eval_consts", air.id == ZKP_AIR_MIMC ? (size_t)ce + 2 : 4 * (size_t)lw + 2);
-    launch_dt_eval_consts(pf, st, air.id, dt_cc, air.k, dt_aval, dz, ce, w, air.num_t, dconst);
-    ec.zinv = air.id == ZKP_AIR_MIMC ? dconst : dz;
-    const std::string dom = std::to_string(logn) + "_" + std::to_string(logB) + "_" + std::to_string(u0) + "_" +
-                            std::to_string(cel);
-    if (air.id == ZKP_AIR_MIMC) {
-      // periodic column K over the CE domain: interpolate over <w_64>, evaluate at g^(n/64) * <w_{64 ce}>
-      // (domain-only: cached per (n, ce))
-      const std::string kkey = "kper_" + std::to_string(logn) + "_" + std::to_string(logce);
-      felt* dk = ctx->buf<felt>(kkey, 64 * (size_t)ce);
-      if (!ctx->have_cached(kkey)) {
-        std::vector<felt> kc(64);
-        for (int j = 0; j < 64; j++) kc[j] = felt_u64((uint64_t)(j + 1) * 1000000ull);
-        host_interpolate(kc, one());
-        std::vector<felt> kv = host_evaluate(kc, 64 * ce, pow_u64(g, n / 64));
-        ctx->upload(dk, kv.data(), kv.size() * 16);
-      }
-      MimcEvalArgs ma;
-      ma.bcoef = dconst + ce;  // b0, b1
-      ma.v0 = air.a_val[0];
-      ma.v1 = air.a_val[1];
-      ma.kper = dk;
-      // divisor inverses depend only on the domain and the assertion steps: cache per config
-      std::string key = "binv_mimc_" + dom;
-      ma.binv_ready = ctx->have_cached(key);
-      ma.binv = ctx->buf<felt>("binv_scratch", ((uint64_t)cel * n) / 2048 + 1);
-      ma.dinv = ctx->buf<felt>(key, (uint64_t)cel * n);
-      launch_eval_mimc(pf, st, ec, ma, tlde, comp);
-    } else if (air.id == ZKP_AIR_GLOBAL_UPDATE) {
-      // GlobalUpdate: T = sum_i a^i (k*next_i - k*cur_i - next_{i+60}); B = sum_c b_c (cur_c - v_c)
-      LinearEvalArgs la;
-      la.width = w;
-      la.transition = true;
-      la.two_groups = false;
-      la.coefs = dconst;  // [next | cur | beta0 | beta1 | bconst0, bconst1]
-      la.w_bstep = pow_u64(wn, air.a_step[0]);
-      la.w_bstep1 = zero();
-      std::string key = "binv_lin_" + dom + "_" + std::to_string(air.a_step[0]);
-      la.binv_ready = ctx->have_cached(key);
-      la.binv = ctx->buf<felt>("binv_scratch", ((uint64_t)cel * n) / 2048 + 1);
-      la.dinv = ctx->buf<felt>(key, (uint64_t)cel * n);
-      launch_eval_linear(pf, st, ec, la, tlde, comp);
-    } else {
-      // TrainingUpdate: transitions identically zero; boundary groups at rows 0 and n-1 over
-      // the masked columns 0..w/2 (the mask columns are never read)
-      const uint32_t half = w / 2;
-      LinearEvalArgs la;
-      la.width = half;
-      la.transition = false;
-      la.two_groups = true;
-      la.coefs = dconst;
-      la.w_bstep = one();
-      la.w_bstep1 = ec.w_last;
-      std::string key = "binv_tu_" + dom;
-      la.binv_ready = ctx->have_cached(key);
-      la.binv = ctx->buf<felt>("binv_scratch", ((uint64_t)cel * n) / 2048 + 1);
-      la.dinv = ctx->buf<felt>(key, (uint64_t)cel * n);
-      launch_eval_linear(pf, st, ec, la, tlde, comp);
-    }
-  }
+  if (cel) constraint_eval(ctx, air, logn, logB, logce, u0, cel, j0, logBl, cx, twn, dt_cc, dt_aval, tlde, comp);
 
   // 4. composition polynomial + commitment (CompositionPoly::new +
   // DefaultConstraintCommitment): per-CE-coset interpolation, exchange of
@@ -724,14 +979,7 @@ int prove_impl(zkp_ctx* ctx, zkp_comm* cm, int air_id, const felt* d_trace, uint
     uint64_t D = N, maxrem = (uint64_t)(o->fri_remainder_max_degree + 1) * B;
     while (D > maxrem) { D /= F; L++; }
   }
-  struct Layer {
-    felt* E;
-    uint64_t m;    // positions per coset
-    uint32_t Bc, jc;
-    bool sharded;
-    TreeShard tree;
-  };
-  std::vector<Layer> layers(L + 1);
+  std::vector<FriLayer> layers(L + 1);
   std::vector<felt> remainder;
   bool dev_tail = false;  // remainder + first grinding chunk on the device
   felt* rem_d = nullptr;
@@ -743,15 +991,7 @@ int prove_impl(zkp_ctx* ctx, zkp_comm* cm, int air_id, const felt* d_trace, uint
     uint64_t tot_e = 0, D = N;
     for (uint32_t l = 0; l < L; l++) { tot_e += D / F; D /= F; }
     felt* fe = ctx->buf<felt>("fri_evals", tot_e + 1);
-    felt* deps = ctx->buf<felt>("eps_inv", 9);
-    if (!ctx->have_cached("eps_inv")) {  // constants of the fold-16 iDFT
-      std::vector<felt> eps(9);
-      felt einv = inv(root_of_unity(4));
-      eps[0] = one();
-      for (int m = 1; m < 8; m++) eps[m] = mul(eps[m - 1], einv);
-      eps[8] = inv(felt_u64(16));
-      ctx->upload(deps, eps.data(), 9 * 16);
-    }
+    const felt* deps = fold_constants(ctx);
     felt* E = deep;
     uint64_t m = n, eo = 0;
     uint32_t Bc = Bl, jc = j0;
@@ -775,7 +1015,7 @@ int prove_impl(zkp_ctx* ctx, zkp_comm* cm, int air_id, const felt* d_trace, uint
     for (uint32_t l = 0; l < L; l++) {
       const uint64_t m16 = m / F;
       if (sh && (m16 >> logR) < 16) replicate(l);
-      Layer& ly = layers[l];
+      FriLayer& ly = layers[l];
       ly.E = E; ly.m = m; ly.Bc = Bc; ly.jc = jc; ly.sharded = sh;
       // sharded layers assemble the root on the host (top levels); it is staged back for the coin
       MerkleTail coin{};
@@ -930,155 +1170,9 @@ int prove_impl(zkp_ctx* ctx, zkp_comm* cm, int air_id, const felt* d_trace, uint
   for (uint64_t i = 0; i < np; i++) T.query_positions[i] = pos[i];
   T.num_composition_columns = C;
 
-  // Openings: every item is (owner rank, local index) or a host-side top node.
-  // Each rank gathers all items from its own memory (index 0 for items it does
-  // not own), the gathered buffers are all-gathered, and every item is taken
-  // from its owner's copy.
-  struct SegPlan {
-    const void* src;
-    std::vector<uint64_t> idx;
-    std::vector<int32_t> owner;  // -1: host top node (value in host_dig)
-    std::vector<const uint8_t*> host_dig;
-    uint32_t words;
-  };
-  auto row_owner = [&](uint64_t j) -> uint32_t { return R > 1 ? (uint32_t)(j / Bl) : 0; };
-  auto lde_values = [&](const felt* src, uint32_t cols) {
-    SegPlan sp{src, {}, {}, {}, 4};
-    sp.idx.reserve(pos.size() * cols);
-    sp.owner.reserve(pos.size() * cols);
-    sp.host_dig.reserve(pos.size() * cols);
-    for (uint64_t p : pos) {
-      uint64_t j = p & (B - 1), t = p >> logB;
-      uint32_t ow = row_owner(j);
-      for (uint32_t c = 0; c < cols; c++) {
-        sp.idx.push_back(ow == rank ? ((uint64_t)c * Bl + (j - j0)) * n + t : 0);
-        sp.owner.push_back((int32_t)ow);
-        sp.host_dig.push_back(nullptr);
-      }
-    }
-    return sp;
-  };
-  auto path_nodes = [&](const TreeShard& tr, const BatchPlan& bp) {
-    SegPlan sp{tr.nodes, {}, {}, {}, 8};
-    for (auto& pth : bp.paths)
-      for (uint64_t k : pth) {
-        TreeShard::Loc lc = tr.locate(k);
-        if (lc.host) {
-          sp.idx.push_back(0);
-          sp.owner.push_back(-1);
-          sp.host_dig.push_back(tr.top[lc.local].data());
-        } else {
-          sp.idx.push_back(lc.owner == (tr.logR ? rank : 0u) ? lc.local : 0);
-          sp.owner.push_back(tr.logR ? (int32_t)lc.owner : (int32_t)rank);
-          sp.host_dig.push_back(nullptr);
-        }
-      }
-    return sp;
-  };
-  const BatchPlan bt = plan_batch(N, pos);
-  const BatchPlan& bc = bt;  // the constraint tree has the same shape and positions
-  std::vector<std::vector<uint64_t>> fpos(L);
-  std::vector<BatchPlan> bf(L);
-  std::vector<SegPlan> plan;
-  plan.push_back(lde_values(tlde, w));
-  plan.push_back(path_nodes(ttree, bt));
-  plan.push_back(lde_values(clde, C));
-  plan.push_back(path_nodes(ctree, bc));
-  {
-    std::vector<uint64_t> cur = pos;
-    for (uint32_t l = 0; l < L; l++) {
-      const Layer& ly = layers[l];
-      const uint64_t m16 = ly.m / F, Rows = (uint64_t)B * m16;
-      fpos[l] = fold_positions(cur, Rows);
-      bf[l] = plan_batch(Rows, fpos[l]);
-      SegPlan sp{ly.E, {}, {}, {}, 4};
-      for (uint64_t r : fpos[l])
-        for (uint32_t k = 0; k < F; k++) {
-          uint64_t i = r + k * Rows;  // natural index in the layer
-          uint64_t j = i & (B - 1), tt = i >> logB;
-          uint32_t ow = ly.sharded ? (uint32_t)(j / Bl) : rank;
-          sp.idx.push_back(ow == rank ? (j - ly.jc) * ly.m + tt : 0);
-          sp.owner.push_back((int32_t)ow);
-          sp.host_dig.push_back(nullptr);
-        }
-      plan.push_back(sp);
-      plan.push_back(path_nodes(ly.tree, bf[l]));
-      cur = fpos[l];
-    }
-  }
-  std::vector<GatherSeg> segs;
-  std::vector<uint64_t> all_idx;
-  uint64_t out_words = 0, max_count = 1;
-  for (auto& sp : plan) {
-    GatherSeg gs;
-    gs.src = sp.src;
-    gs.idx_off = all_idx.size();
-    gs.count = sp.idx.size();
-    gs.out_off = out_words;
-    gs.words = sp.words;
-    gs.pad = 0;
-    all_idx.insert(all_idx.end(), sp.idx.begin(), sp.idx.end());
-    out_words += gs.count * sp.words;
-    max_count = std::max<uint64_t>(max_count, gs.count);
-    segs.push_back(gs);
-  }
-  size_t seg_bytes = segs.size() * sizeof(GatherSeg), idx_bytes = all_idx.size() * 8;
-  size_t up_bytes = seg_bytes + idx_bytes, down_bytes = out_words * 4;
-  ctx->stage_end("7a_query_plan");
-  uint8_t* hp = (uint8_t*)ctx->pinned(std::max(up_bytes, down_bytes * R) + 64);
-  memcpy(hp, segs.data(), seg_bytes);
-  memcpy(hp + seg_bytes, all_idx.data(), idx_bytes);
-  uint8_t* dup = ctx->buf<uint8_t>("gather_in", up_bytes + 16);
-  uint32_t* dout = ctx->buf<uint32_t>("gather_out", out_words + 4);
-  uint32_t* dall = R > 1 ? ctx->buf<uint32_t>("gather_all", out_words * R + 4) : dout;
-  HIP_CHECK(hipMemcpyAsync(dup, hp, up_bytes, hipMemcpyHostToDevice, st));
-  launch_gather_multi(pf, st, (const GatherSeg*)dup, (uint32_t)segs.size(), max_count,
-                      (const uint64_t*)(dup + seg_bytes), dout, (double)down_bytes * 2);
-  if (R > 1) cm->all_gather(st, dout, dall, down_bytes);
-  HIP_CHECK(hipMemcpyAsync(hp, dall, down_bytes * R, hipMemcpyDeviceToHost, st));
-  ctx->sync();
-  ctx->stage_end("7b_gather");
-  std::vector<uint32_t> gathered(out_words);
-  {
-    const uint32_t* all = reinterpret_cast<const uint32_t*>(hp);
-    for (size_t si = 0; si < plan.size(); si++) {
-      const SegPlan& sp = plan[si];
-      const GatherSeg& gs = segs[si];
-      for (size_t it = 0; it < sp.idx.size(); it++) {
-        uint32_t* dst = gathered.data() + gs.out_off + it * sp.words;
-        if (sp.owner[it] < 0) {
-          memcpy(dst, sp.host_dig[it], 32);
-        } else {
-          uint32_t ow = R > 1 ? (uint32_t)sp.owner[it] : 0;
-          memcpy(dst, all + (size_t)ow * out_words + gs.out_off + it * sp.words, sp.words * 4);
-        }
-      }
-    }
-  }
-  size_t seg_cursor = 0;
-  // values and batch paths are written straight from the gathered words
-  // (felts are stored canonical LE, i.e. already in their wire format)
-  auto write_values = [&](Writer& wr) {
-    const GatherSeg& gs = segs[seg_cursor++];
-    wr.u32((uint32_t)(gs.count * 16));
-    wr.put(gathered.data() + gs.out_off, gs.count * 16);
-  };
-  auto write_batch = [&](Writer& wr, const BatchPlan& bp) {
-    const GatherSeg& gs = segs[seg_cursor++];
-    const uint32_t* d = gathered.data() + gs.out_off;
-    size_t nodes = 0;
-    for (auto& p : bp.paths) nodes += p.size();
-    wr.u32((uint32_t)(2 + bp.paths.size() + 32 * nodes));
-    wr.u8((uint8_t)bp.depth);
-    wr.u8((uint8_t)bp.paths.size());
-    size_t k = 0;
-    for (auto& p : bp.paths) {
-      wr.u8((uint8_t)p.size());
-      wr.put(d + 8 * k, 32 * p.size());
-      k += p.size();
-    }
-  };
-
+  Openings op;
+  gather_openings(ctx, cm, pos, n, logB, j0, tlde, w, ttree, clde, C, ctree, layers, L, F, op);
+  const uint64_t out_words = op.gathered.size();
   // 10. serialize (≙ Proof::to_bytes)
   Writer wr;
   wr.b.reserve((size_t)out_words * 4 + 64 * (size_t)(L + 4) + 32 * (size_t)(w + C) + 16 * remainder.size() + 4096);
@@ -1090,20 +1184,14 @@ int prove_impl(zkp_ctx* ctx, zkp_comm* cm, int air_id, const felt* d_trace, uint
   for (uint32_t l = 0; l < L; l++) wr.put(T.fri_roots[l], 32);
   wr.put(T.remainder_commitment, 32);
   wr.u8(1);
-  for (int seg = 0; seg < 2; seg++) {
-    write_values(wr);
-    write_batch(wr, seg == 0 ? bt : bc);
-  }
+  op.write_commitment_queries(wr);
   wr.u16((uint16_t)(1 + 16 * 2 * w));
   wr.u8(2);
   for (felt v : ood_trace) wr.fe(v);
   wr.u16((uint16_t)(16 * C));
   for (felt v : ood_comp) wr.fe(v);
   wr.u8((uint8_t)L);
-  for (uint32_t l = 0; l < L; l++) {
-    write_values(wr);
-    write_batch(wr, bf[l]);
-  }
+  op.write_fri_queries(wr);
   wr.u16((uint16_t)(16 * remainder.size()));
   for (felt v : remainder) wr.fe(v);
   wr.u8(1);
@@ -1482,6 +1570,340 @@ int zkp_build_mimc_trace(const uint8_t seed[16], uint64_t n, zkp_felt* out) {
     v = mul(u6, u);
   }
   return 0;
+}
+
+}  // extern "C"
+
+// ====================================================================== stage sessions
+// The stage entry points of include/zkp.h: one proof's
+// device-resident state, driven stage by stage by a caller that keeps its own
+// Fiat-Shamir channel (a winter-prover 0.12 fork keeping `Prover::prove`).
+// Same kernels as zkp_prove; the coin draws come from the caller instead of
+// the device transcript. World 1 (one GPU).
+struct zkp_session {
+  zkp_ctx* ctx = nullptr;
+  AirDesc air;
+  zkp_proof_options o{};
+  uint32_t w = 0, B = 0, ce = 0, C = 0, F = 16, L = 0;
+  uint32_t logn = 0, logB = 0, logce = 0, logN = 0;
+  uint64_t n = 0, N = 0;
+  int stage = 0;  // 1 trace committed, 2 evaluated, 3 composition committed, 4 OOD, 5 DEEP/FRI done
+  std::string pfx;
+  TreeShard ttree, ctree;
+  std::vector<FriLayer> layers;
+  felt z{}, zg{};
+  std::vector<felt> ood;  // [2a + {0,1}]: array a (trace columns, then composition columns) at z, zg
+
+  template <typename T>
+  T* buf(const char* name, size_t count) { return ctx->buf<T>(pfx + name, count); }
+  felt* get(const char* name) { return reinterpret_cast<felt*>(ctx->bufs[pfx + name].p); }
+  void begin(int need) {
+    if (stage != need) throw ZkpFail{ZKP_ERR_ARGUMENT, "stage entry point called out of order"};
+    HIP_CHECK(hipSetDevice(ctx->device));
+    ctx->sync();
+    ctx->ring_reset();
+  }
+};
+
+namespace {
+
+template <typename Fn>
+int session_guard(zkp_session* s, Fn&& f) {
+  if (!s) return ZKP_ERR_ARGUMENT;
+  return guarded(s->ctx, [&] {
+    s->ctx->err.clear();
+    int rc = f();
+    s->ctx->collect_prof();
+    return rc;
+  });
+}
+
+}  // namespace
+
+extern "C" {
+
+int zkp_session_create(zkp_ctx* ctx, zkp_air_id air_id, uint32_t width, uint64_t n, const zkp_felt* pub_elems,
+                       uint64_t n_pub, const zkp_proof_options* o, zkp_session** out) {
+  return guarded(ctx, [&] {
+    if (!out) return (int)ZKP_ERR_ARGUMENT;
+    *out = nullptr;
+    int rc = check_options(o);
+    if (rc) return rc;
+    if (n < 8 || (n & (n - 1)) || width == 0 || width > 255) return (int)ZKP_ERR_TRACE_SHAPE;
+    if (n_pub && !pub_elems) return (int)ZKP_ERR_ARGUMENT;
+    std::vector<felt> pub(n_pub);
+    for (uint64_t i = 0; i < n_pub; i++) pub[i] = make(pub_elems[i].lo, pub_elems[i].hi);
+    auto s = std::make_unique<zkp_session>();
+    rc = build_air(s->air, air_id, width, n, pub);
+    if (rc) return rc;
+    s->ctx = ctx;
+    s->o = *o;
+    s->w = width; s->n = n; s->B = o->blowup_factor; s->F = o->fri_folding_factor;
+    s->ce = s->air.ce_blowup(); s->C = s->air.comp_cols();
+    if (s->B < s->ce) return (int)ZKP_ERR_INVALID_OPTIONS;
+    if (s->ce > 16 || s->C > s->ce) return (int)ZKP_ERR_UNSUPPORTED_AIR;
+    s->logn = ilog2(n); s->logB = ilog2(s->B); s->logce = ilog2(s->ce); s->logN = s->logn + s->logB;
+    s->N = n << s->logB;
+    if (s->logN > 32) return (int)ZKP_ERR_TRACE_SHAPE;
+    uint64_t D = s->N, maxrem = (uint64_t)(o->fri_remainder_max_degree + 1) * s->B;
+    while (D > maxrem) { D /= s->F; s->L++; }
+    s->pfx = "sess" + std::to_string(ctx->next_session++) + "_";
+    *out = s.release();
+    return 0;
+  });
+}
+
+void zkp_session_destroy(zkp_session* s) {
+  if (!s) return;
+  (void)guarded(s->ctx, [&] {
+    HIP_CHECK(hipSetDevice(s->ctx->device));
+    s->ctx->drop(s->pfx);
+    return 0;
+  });
+  delete s;
+}
+
+int zkp_session_trace_lde(zkp_session* s, const zkp_felt* trace_cols, uint8_t root[32]) {
+  return session_guard(s, [&] {
+    if (!trace_cols || !root) return (int)ZKP_ERR_ARGUMENT;
+    s->begin(0);
+    zkp_ctx* ctx = s->ctx;
+    const uint64_t n = s->n;
+    felt* d = s->buf<felt>("trace", (size_t)s->w * n);
+    ctx->upload(d, trace_cols, (size_t)s->w * n * 16);
+    ctx->ensure_coset(s->logn, s->logB, s->logce);
+    felt* coef = s->buf<felt>("coef", (size_t)(s->w + s->C) * n);
+    felt* tlde = s->buf<felt>("tlde", (size_t)s->w * s->N);
+    NttBatch ib{d, coef, nullptr, n, n, 1, 1, s->w};
+    launch_ntt(ctx->prof, ctx->stream, ib, s->logn, false, ctx->itws(s->logN), s->logN);
+    NttBatch lb{coef, tlde, ctx->S(s->logn, s->logB), n, n, s->B, s->B, s->w * s->B};
+    launch_ntt(ctx->prof, ctx->stream, lb, s->logn, true, ctx->tws(s->logN), s->logN);
+    commit_rows(ctx, ctx->self_comm(), 0, tlde, n, s->w, s->logB, s->logn, false, s->pfx + "ttree", s->ttree, root);
+    s->stage = 1;
+    return 0;
+  });
+}
+
+int zkp_eval_constraints(zkp_session* s, const zkp_felt* coeffs, uint32_t n_coeffs, zkp_felt* evals_out) {
+  return session_guard(s, [&] {
+    if (!coeffs) return (int)ZKP_ERR_ARGUMENT;
+    s->begin(1);
+    zkp_ctx* ctx = s->ctx;
+    const AirDesc& air = s->air;
+    if (n_coeffs != air.num_t + air.a_col.size()) return (int)ZKP_ERR_ARGUMENT;
+    felt* dcc = s->buf<felt>("cc", n_coeffs);
+    ctx->upload(dcc, coeffs, (size_t)n_coeffs * 16);
+    felt* daval = s->buf<felt>("aval", air.a_val.size());
+    ctx->upload(daval, air.a_val.data(), air.a_val.size() * 16);
+    felt* cx = coset_points(ctx, s->logn, s->logB, s->logce);
+    const felt* twn = ctx->tws(s->logN) + ((1ull << (s->logn - 1)) - 1);
+    felt* comp = s->buf<felt>("comp", (size_t)s->ce * s->n);
+    constraint_eval(ctx, air, s->logn, s->logB, s->logce, 0, s->ce, 0, s->logB, cx, twn, dcc, daval, s->get("tlde"),
+                    comp);
+    if (evals_out) {  // CE-coset-major on the device -> natural CE domain order
+      std::vector<felt> h((size_t)s->ce * s->n);
+      ctx->download(h.data(), comp, h.size() * 16);
+      for (uint32_t u = 0; u < s->ce; u++)
+        for (uint64_t t = 0; t < s->n; t++) {
+          const felt v = h[(size_t)u * s->n + t];
+          evals_out[u + (size_t)s->ce * t] = zkp_felt{v.lo, v.hi};
+        }
+    }
+    ctx->sync();
+    s->stage = 2;
+    return 0;
+  });
+}
+
+int zkp_composition_commit(zkp_session* s, const zkp_felt* evals, uint8_t root[32], uint32_t* num_columns) {
+  return session_guard(s, [&] {
+    if (!root) return (int)ZKP_ERR_ARGUMENT;
+    if (evals && s->stage == 1) s->stage = 2;  // caller-evaluated constraints (natural CE order)
+    s->begin(2);
+    zkp_ctx* ctx = s->ctx;
+    Prof& pf = ctx->prof;
+    hipStream_t st = ctx->stream;
+    const uint64_t n = s->n;
+    const uint32_t ce = s->ce, C = s->C;
+    felt* comp = s->buf<felt>("comp", (size_t)ce * n);
+    if (evals) {
+      std::vector<felt> h((size_t)ce * n);
+      for (uint32_t u = 0; u < ce; u++)
+        for (uint64_t t = 0; t < n; t++) {
+          const zkp_felt& v = evals[u + (size_t)ce * t];
+          h[(size_t)u * n + t] = make(v.lo, v.hi);
+          if (ge_p(h[(size_t)u * n + t])) throw ZkpFail{ZKP_ERR_ARGUMENT, "non-canonical evaluation"};
+        }
+      ctx->upload(comp, h.data(), h.size() * 16);
+    }
+    NttBatch ib{comp, comp, nullptr, n, n, 1, 1, ce};
+    launch_ntt(pf, st, ib, s->logn, false, ctx->itws(s->logN), s->logN);
+    const std::string dkey = "comp_dft_" + std::to_string(s->logn) + "_" + std::to_string(s->logce) + "_" +
+                             std::to_string(C) + "_1_" + std::to_string(ce);
+    felt* dcoefs = ctx->buf<felt>(dkey + "_coefs", (size_t)ce * C);
+    uint32_t* dblk = ctx->buf<uint32_t>(dkey + "_blk", ce);
+    if (!ctx->have_cached(dkey)) {  // world 1: blk[u] = u (same table as zkp_prove's)
+      std::vector<felt> dc((size_t)ce * C);
+      const felt g = felt_u64(3);
+      felt wce_inv = inv(root_of_unity(s->logce)), ce_inv = inv(felt_u64(ce)), gn_inv = inv(pow_u64(g, n));
+      for (uint32_t u = 0; u < ce; u++)
+        for (uint32_t m = 0; m < C; m++)
+          dc[(size_t)u * C + m] = mul(mul(pow_u64(wce_inv, (uint64_t)u * m), pow_u64(gn_inv, m)), ce_inv);
+      std::vector<uint32_t> blk(ce);
+      for (uint32_t u = 0; u < ce; u++) blk[u] = u;
+      ctx->upload(dcoefs, dc.data(), dc.size() * 16);
+      ctx->upload(dblk, blk.data(), blk.size() * 4);
+    }
+    felt* acoef = s->get("coef") + (size_t)s->w * n;
+    launch_comp_dft(pf, st, comp, dblk, ctx->Si(s->logn, s->logB, s->logce), dcoefs, ce, C, s->logn, 0, n, acoef);
+    felt* clde = s->buf<felt>("clde", (size_t)C * s->N);
+    NttBatch lb{acoef, clde, ctx->S(s->logn, s->logB), n, n, s->B, s->B, C * s->B};
+    launch_ntt(pf, st, lb, s->logn, true, ctx->tws(s->logN), s->logN);
+    commit_rows(ctx, ctx->self_comm(), 0, clde, n, C, s->logB, s->logn, false, s->pfx + "ctree", s->ctree, root);
+    if (num_columns) *num_columns = C;
+    s->stage = 3;
+    return 0;
+  });
+}
+
+int zkp_ood_frame(zkp_session* s, zkp_felt zf, zkp_felt* trace_ood, zkp_felt* comp_ood) {
+  return session_guard(s, [&] {
+    if (!trace_ood || !comp_ood) return (int)ZKP_ERR_ARGUMENT;
+    s->begin(3);
+    zkp_ctx* ctx = s->ctx;
+    s->z = make(zf.lo, zf.hi);
+    if (ge_p(s->z)) return (int)ZKP_ERR_ARGUMENT;
+    s->zg = mul(s->z, root_of_unity(s->logn));
+    std::vector<felt> pw(2 * (size_t)s->logn);
+    felt a = s->z, b = s->zg;
+    for (uint32_t l = 0; l < s->logn; l++) { pw[l] = a; pw[s->logn + l] = b; a = sqr(a); b = sqr(b); }
+    felt* dpw = s->buf<felt>("pw", pw.size());
+    ctx->upload(dpw, pw.data(), pw.size() * 16);
+    felt* dv = ood_launch(ctx, s->get("coef"), s->w + s->C, s->w, s->logn, dpw);
+    s->ood.resize(2 * (size_t)(s->w + s->C));
+    ctx->download(s->ood.data(), dv, s->ood.size() * 16);
+    for (uint32_t c = 0; c < s->w; c++) {
+      trace_ood[c] = zkp_felt{s->ood[2 * c].lo, s->ood[2 * c].hi};
+      trace_ood[s->w + c] = zkp_felt{s->ood[2 * c + 1].lo, s->ood[2 * c + 1].hi};
+    }
+    for (uint32_t h = 0; h < s->C; h++) comp_ood[h] = zkp_felt{s->ood[2 * (s->w + h)].lo, s->ood[2 * (s->w + h)].hi};
+    s->stage = 4;
+    return 0;
+  });
+}
+
+int zkp_deep_fri(zkp_session* s, const zkp_felt* deep_coeffs, zkp_fri_channel channel, void* user,
+                 zkp_felt* remainder, uint64_t* remainder_len, uint8_t remainder_commitment[32]) {
+  return session_guard(s, [&] {
+    if (!deep_coeffs || !channel || !remainder_len || !remainder_commitment) return (int)ZKP_ERR_ARGUMENT;
+    s->begin(4);
+    zkp_ctx* ctx = s->ctx;
+    Prof& pf = ctx->prof;
+    hipStream_t st = ctx->stream;
+    const uint32_t w = s->w, C = s->C, B = s->B, F = s->F;
+    const uint64_t n = s->n;
+    const felt g = felt_u64(3);
+    // DEEP coefficients and the OOD combinations kz = sum gamma_i T_i(z) (+ composition), kzg
+    std::vector<felt> gam(w + C), dkh(4);
+    for (uint32_t i = 0; i < w + C; i++) gam[i] = make(deep_coeffs[i].lo, deep_coeffs[i].hi);
+    felt kz = zero(), kzg = zero();
+    for (uint32_t c = 0; c < w; c++) {
+      kz = add(kz, mul(gam[c], s->ood[2 * c]));
+      kzg = add(kzg, mul(gam[c], s->ood[2 * c + 1]));
+    }
+    for (uint32_t h = 0; h < C; h++) kz = add(kz, mul(gam[w + h], s->ood[2 * (w + h)]));
+    dkh[0] = s->z; dkh[1] = s->zg; dkh[2] = kz; dkh[3] = kzg;
+    felt* dgam = s->buf<felt>("gamma", w + C);
+    felt* dk = s->buf<felt>("dk", 4);
+    ctx->upload(dgam, gam.data(), gam.size() * 16);
+    ctx->upload(dk, dkh.data(), 64);
+    felt* cx = coset_points(ctx, s->logn, s->logB, s->logce);
+    const felt* twn = ctx->tws(s->logN) + ((1ull << (s->logn - 1)) - 1);
+    const PointMap pm{cx, twn, s->logn};
+    felt* binv = s->buf<felt>("binv", s->N / 2048 + 1);
+    launch_deep_denominators(pf, st, pm, s->N, dk, s->get("pw"), binv);
+    felt* deep = s->buf<felt>("deep", s->N);
+    DeepArgs da;
+    da.w = w; da.C = C; da.logB = s->logB; da.logn = s->logn; da.logN = s->logN;
+    da.j0 = 0; da.logBl = s->logB;
+    da.tlde = s->get("tlde"); da.clde = s->get("clde"); da.gamma = dgam; da.dk = dk; da.g = g;
+    da.pm = pm;
+    da.binv = binv;
+    launch_deep(pf, st, da, deep);
+    // FriProver::build_layers: commit each layer, the caller's channel returns alpha, fold
+    s->layers.assign(s->L + 1, FriLayer{});
+    uint64_t tot = 0, D = s->N;
+    for (uint32_t l = 0; l < s->L; l++) { tot += D / F; D /= F; }
+    felt* fe = s->buf<felt>("fri_evals", tot + 1);
+    felt* alphas = s->buf<felt>("alphas", s->L + 1);
+    const felt* deps = fold_constants(ctx);
+    felt* E = deep;
+    uint64_t m = n, eo = 0;
+    felt off = g;
+    D = s->N;
+    for (uint32_t l = 0; l < s->L; l++) {
+      const uint64_t m16 = m / F;
+      FriLayer& ly = s->layers[l];
+      ly.E = E; ly.m = m; ly.Bc = B; ly.jc = 0; ly.sharded = false;
+      uint8_t root[32];
+      commit_rows(ctx, ctx->self_comm(), 1, E, 0, F, s->logB, ilog2(m16), false, s->pfx + "ftree_" + std::to_string(l),
+                  ly.tree, root);
+      zkp_felt af{0, 0};
+      if (channel(user, l, root, &af) != 0) throw ZkpFail{ZKP_ERR_ARGUMENT, "FRI channel callback failed"};
+      felt alpha = make(af.lo, af.hi);
+      if (ge_p(alpha)) throw ZkpFail{ZKP_ERR_ARGUMENT, "non-canonical FRI alpha"};
+      ctx->upload(alphas + l, &alpha, 16);
+      felt* nxt = fe + eo;
+      launch_fri_fold(pf, st, E, m16, B, 0, s->logB, F, alphas + l, inv(off), ctx->itws(s->logN), ilog2(D), deps, nxt);
+      eo += (uint64_t)B * m16;
+      E = nxt;
+      m = m16;
+      D /= F;
+      off = pow_u64(off, F);
+    }
+    s->layers[s->L].E = E; s->layers[s->L].m = m; s->layers[s->L].Bc = B;
+    // FriProver::set_remainder: interpolate the last layer (coset-major -> natural), keep D/B coefficients
+    std::vector<felt> last((size_t)B * m), rem(D);
+    ctx->download(last.data(), E, last.size() * 16);
+    for (uint64_t j = 0; j < B; j++)
+      for (uint64_t t = 0; t < m; t++) rem[j + B * t] = last[j * m + t];
+    host_interpolate(rem, off);
+    rem.resize(D / B);
+    hash_elements(rem.data(), rem.size(), remainder_commitment);
+    if (remainder) {
+      if (*remainder_len < rem.size()) return (int)ZKP_ERR_ARGUMENT;
+      for (size_t i = 0; i < rem.size(); i++) remainder[i] = zkp_felt{rem[i].lo, rem[i].hi};
+    }
+    *remainder_len = rem.size();
+    s->stage = 5;
+    return 0;
+  });
+}
+
+int zkp_query(zkp_session* s, const uint64_t* positions, uint64_t n_positions, uint8_t** out, uint64_t* out_len) {
+  return session_guard(s, [&] {
+    if (!positions || !out || !out_len || n_positions == 0 || n_positions > 255) return (int)ZKP_ERR_ARGUMENT;
+    s->begin(5);
+    std::vector<uint64_t> pos(positions, positions + n_positions);
+    for (uint64_t i = 0; i < n_positions; i++)
+      if (pos[i] >= s->N || (i && pos[i] <= pos[i - 1])) return (int)ZKP_ERR_ARGUMENT;  // sorted, unique, in range
+    zkp_ctx* ctx = s->ctx;
+    Openings op;
+    gather_openings(ctx, ctx->self_comm(), pos, s->n, s->logB, 0, s->get("tlde"), s->w, s->ttree, s->get("clde"), s->C,
+                    s->ctree, s->layers, s->L, s->F, op);
+    Writer wr;
+    wr.u8(1);  // one trace segment
+    op.write_commitment_queries(wr);
+    wr.u8((uint8_t)s->L);
+    op.write_fri_queries(wr);
+    uint8_t* p = (uint8_t*)malloc(wr.b.size());
+    if (!p) return (int)ZKP_ERR_OOM;
+    memcpy(p, wr.b.data(), wr.b.size());
+    *out = p;
+    *out_len = wr.b.size();
+    s->stage = 5;  // queries may be asked again (e.g. after a re-grind)
+    return 0;
+  });
 }
 
 }  // extern "C"
