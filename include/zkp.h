@@ -146,6 +146,22 @@ int zkp_comm_rccl_create(zkp_ctx* ctx, const uint8_t id[128], int world, int ran
 /* In-process group: `world` communicators for ranks run as threads of one
  * process (each with its own zkp_ctx; GPUs may be shared). comms[world]. */
 int zkp_comm_local_group(int world, zkp_comm** comms);
+/* Caller transport: one process per rank, the collectives carried by the
+ * caller's own channel (torch.distributed/gloo, MPI, sockets ...) through pinned
+ * host staging. Each callback is a blocking collective over all ranks that
+ * returns 0 on success: all_to_all sends block s of `send` (block_bytes each) to
+ * rank s and receives rank s's block for this rank into block s of `recv`;
+ * all_gather puts rank s's `send` (bytes) at recv + s*bytes. abort (nullable)
+ * is called when this rank's proof fails, to release blocked peers. The
+ * exchange points are those of the RCCL backend; RCCL stays the production
+ * transport over xGMI. */
+typedef struct zkp_host_transport {
+  void* user;
+  int (*all_to_all)(void* user, const void* send, void* recv, uint64_t block_bytes);
+  int (*all_gather)(void* user, const void* send, void* recv, uint64_t bytes);
+  void (*abort)(void* user);
+} zkp_host_transport;
+int zkp_comm_host_create(int world, int rank, const zkp_host_transport* transport, zkp_comm** out);
 void zkp_comm_destroy(zkp_comm* comm);
 int zkp_comm_rank(const zkp_comm* comm);
 int zkp_comm_world(const zkp_comm* comm);

@@ -39,3 +39,60 @@ def test_two_rank_rccl_id_broadcast_gloo():
     for r in range(world):
         uid, w, rr = out[r]
         assert uid == want and w == world and rr == r
+
+
+def _transport_worker(rank, world, port, out):
+    """Drives the gloo caller transport through the same C function pointers
+    (zkp_host_transport) the library calls, on pinned-like host buffers."""
+    import ctypes
+
+    import numpy as np
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from zk_stark_project_amd import _native, sharded
+    a2a, ag = sharded.gloo_transport(world)
+    captured = {}
+
+    def fake_create(w, r, tp, outp):  # zkp_comm_host_create stand-in: keep the transport struct
+        captured["t"] = ctypes.cast(tp, ctypes.POINTER(_native.HostTransport))[0]
+        outp._obj.value = 1
+        return 0
+
+    class FakeLib:
+        zkp_comm_host_create = staticmethod(fake_create)
+
+        def zkp_comm_destroy(self, p):
+            pass
+    real_load = _native.load
+    _native.load = lambda: FakeLib()
+    try:
+        comm = _native.host_comm(rank, world, a2a, ag)
+    finally:
+        _native.load = real_load
+    t = captured["t"]
+    block = 40
+    send = np.array([(rank * 100 + s * 10 + i) % 256 for s in range(world) for i in range(block)], dtype=np.uint8)
+    recv = np.zeros(world * block, dtype=np.uint8)
+    rc1 = t.all_to_all(None, send.ctypes.data, recv.ctypes.data, block)
+    mine = np.array([(rank * 7 + i) % 256 for i in range(block)], dtype=np.uint8)
+    gat = np.zeros(world * block, dtype=np.uint8)
+    rc2 = t.all_gather(None, mine.ctypes.data, gat.ctypes.data, block)
+    out[rank] = (rc1, rc2, recv.tobytes(), gat.tobytes())
+    comm.ptr = ctypes.c_void_p()
+    dist.destroy_process_group()
+
+
+def test_two_rank_gloo_caller_transport():
+    """all_to_all: block s of rank r reaches rank s as its block r; all_gather: rank s's
+    buffer lands at block s on every rank (the contract of include/zkp.h)."""
+    world, block = 2, 40
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_transport_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    for r in range(world):
+        rc1, rc2, recv, gat = out[r]
+        assert rc1 == 0 and rc2 == 0
+        want = bytes((s * 100 + r * 10 + i) % 256 for s in range(world) for i in range(block))
+        assert recv == want
+        assert gat == bytes((s * 7 + i) % 256 for s in range(world) for i in range(block))

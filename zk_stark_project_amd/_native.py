@@ -73,8 +73,18 @@ EXPORTED = [
     "zkp_comm_rccl_create", "zkp_comm_destroy", "zkp_comm_rank", "zkp_comm_world", "zkp_prove_sharded_device",
     "zkp_verify", "zkp_build_global_update_trace", "zkp_set_profiling_kernel",
     "zkp_session_create", "zkp_session_destroy", "zkp_session_trace_lde", "zkp_eval_constraints",
-    "zkp_composition_commit", "zkp_ood_frame", "zkp_deep_fri", "zkp_query",
+    "zkp_composition_commit", "zkp_ood_frame", "zkp_deep_fri", "zkp_query", "zkp_comm_host_create",
 ]
+
+# zkp_host_transport callbacks (include/zkp.h)
+HOST_A2A = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64)
+HOST_ABORT = ctypes.CFUNCTYPE(None, ctypes.c_void_p)
+
+
+class HostTransport(ctypes.Structure):
+    _fields_ = [("user", ctypes.c_void_p), ("all_to_all", HOST_A2A), ("all_gather", HOST_A2A),
+                ("abort", HOST_ABORT)]
+
 
 # int (*zkp_fri_channel)(void* user, uint32_t layer, const uint8_t root[32], zkp_felt* alpha)
 FRI_CHANNEL = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint8),
@@ -153,6 +163,7 @@ def load():
         L.zkp_verify.argtypes = [i32, ctypes.c_char_p, u64, vp, u64, popt]
         L.zkp_verify.restype = i32
         L.zkp_build_global_update_trace.argtypes = [vp, vp, vp, vp, u64, Felt, u64, vp, vp]
+        L.zkp_comm_host_create.argtypes = [i32, i32, ctypes.POINTER(HostTransport), ctypes.POINTER(vp)]
         L.zkp_session_create.argtypes = [vp, i32, u32, u64, vp, u64, popt, ctypes.POINTER(vp)]
         L.zkp_session_destroy.argtypes = [vp]
         L.zkp_session_destroy.restype = None
@@ -226,6 +237,32 @@ def local_group(world: int) -> list:
     if rc:
         raise ZkpError(rc, "zkp_comm_local_group")
     return [Comm(arr[i]) for i in range(world)]
+
+
+def host_comm(rank: int, world: int, all_to_all, all_gather, abort=None) -> Comm:
+    """`zkp_comm` over a caller transport: all_to_all(send_ptr, recv_ptr, block_bytes) and
+    all_gather(send_ptr, recv_ptr, bytes) are blocking collectives on host memory."""
+    L = load()
+
+    def wrap(fn):
+        def cb(user, send, recv, nbytes):
+            try:
+                fn(send, recv, int(nbytes))
+                return 0
+            except Exception:  # noqa: BLE001 — reported to the library as a failed collective
+                import traceback
+                traceback.print_exc()
+                return 1
+        return HOST_A2A(cb)
+    t = HostTransport(None, wrap(all_to_all), wrap(all_gather),
+                      HOST_ABORT(lambda user: abort() if abort else None))
+    p = ctypes.c_void_p()
+    rc = L.zkp_comm_host_create(world, rank, ctypes.byref(t), ctypes.byref(p))
+    if rc:
+        raise ZkpError(rc, "zkp_comm_host_create")
+    c = Comm(p.value)
+    c._transport = t  # keeps the callbacks alive as long as the communicator
+    return c
 
 
 def rccl_unique_id() -> bytes:

@@ -106,7 +106,56 @@ struct RcclComm : zkp_comm {
   }
 };
 
+// ------------------------------------------------------------------ caller transport
+// One process per rank, collectives carried by the caller's transport
+// (zkp_host_transport: e.g. torch.distributed/gloo, MPI, sockets) through
+// pinned host staging: device -> host, the caller's collective, host -> device.
+// The exchange points and buffers are exactly those of the RCCL backend.
+struct HostComm : zkp_comm {
+  zkp_host_transport t{};
+  void* stage = nullptr;
+  size_t stage_bytes = 0;
+  const char* kind() const override { return "host"; }
+  char* staging(size_t bytes) {
+    if (stage_bytes < bytes) {
+      if (stage) (void)hipHostFree(stage);
+      stage = nullptr;
+      stage_bytes = 0;
+      hip_ok(hipHostMalloc(&stage, bytes, hipHostMallocDefault), "host comm staging");
+      stage_bytes = bytes;
+    }
+    return static_cast<char*>(stage);
+  }
+  void exchange(hipStream_t st, const void* send, void* recv, size_t bytes, bool a2a) {
+    const size_t out_b = a2a ? (size_t)world * bytes : bytes, in_b = (size_t)world * bytes;
+    char* hs = staging(out_b + in_b);
+    char* hr = hs + out_b;
+    if (out_b) hip_ok(hipMemcpyAsync(hs, send, out_b, hipMemcpyDeviceToHost, st), "host comm: D2H");
+    hip_ok(hipStreamSynchronize(st), "host comm: sync before the transport");
+    int rc = a2a ? t.all_to_all(t.user, hs, hr, bytes) : t.all_gather(t.user, hs, hr, bytes);
+    if (rc != 0) throw CommError("caller transport failed (status " + std::to_string(rc) + ")");
+    if (in_b) hip_ok(hipMemcpyAsync(recv, hr, in_b, hipMemcpyHostToDevice, st), "host comm: H2D");
+    hip_ok(hipStreamSynchronize(st), "host comm: sync after H2D");  // staging is reused by the next exchange
+  }
+  void all_to_all(hipStream_t st, const void* send, void* recv, size_t b) override { exchange(st, send, recv, b, true); }
+  void all_gather(hipStream_t st, const void* send, void* recv, size_t b) override { exchange(st, send, recv, b, false); }
+  void abort() override {
+    if (t.abort) t.abort(t.user);
+  }
+  ~HostComm() override {
+    if (stage) (void)hipHostFree(stage);
+  }
+};
+
 }  // namespace
+
+zkp_comm* make_host_comm(int world, int rank, const zkp_host_transport& t) {
+  auto* c = new HostComm();
+  c->rank = rank;
+  c->world = world;
+  c->t = t;
+  return c;
+}
 
 zkp_comm* make_self_comm() { return new SelfComm(); }
 

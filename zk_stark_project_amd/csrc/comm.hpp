@@ -12,6 +12,8 @@
 // ranks sharing one GPU in tests), and RCCL over xGMI (one process per GPU).
 #pragma once
 #include <hip/hip_runtime.h>
+
+#include "../../include/zkp.h"
 #include <stddef.h>
 
 #include <stdexcept>
@@ -34,6 +36,8 @@ struct CommError : std::runtime_error {
 };
 
 zkp_comm* make_self_comm();
+// caller transport through pinned host staging (include/zkp.h zkp_host_transport)
+zkp_comm* make_host_comm(int world, int rank, const zkp_host_transport& t);
 // `world` communicators of one in-process group (out[0..world))
 void make_local_group(int world, zkp_comm** out);
 // RCCL; `id` = NCCL_UNIQUE_ID_BYTES from rccl_unique_id on one rank

@@ -1357,6 +1357,17 @@ int zkp_comm_rccl_create(zkp_ctx* ctx, const uint8_t id[128], int world, int ran
   });
 }
 
+int zkp_comm_host_create(int world, int rank, const zkp_host_transport* t, zkp_comm** out) {
+  if (!t || !out || !t->all_to_all || !t->all_gather || world < 1 || world > 64 || rank < 0 || rank >= world)
+    return ZKP_ERR_ARGUMENT;
+  try {
+    *out = make_host_comm(world, rank, *t);
+  } catch (...) {
+    return ZKP_ERR_OOM;
+  }
+  return ZKP_OK;
+}
+
 void zkp_comm_destroy(zkp_comm* comm) { delete comm; }
 
 int zkp_comm_rank(const zkp_comm* comm) { return comm ? comm->rank : -1; }

@@ -10,11 +10,16 @@ to form the rank group:
 * `rccl_group_comm` — one process per GPU under torchrun; the library's own
   RCCL communicator (xGMI) carries the collectives, torch.distributed only
   broadcasts the 128-byte RCCL unique id.
+* `gloo_group_comm` — one process per rank, the collectives carried by
+  torch.distributed (gloo, host memory) through the library's caller-transport
+  backend (`zkp_comm_host_create`): the same exchange points as RCCL, usable
+  where RCCL is not (several ranks on one GPU, CPU-side transports).
 
 Every rank returns the same proof bytes, identical to `Context.prove`'s.
 """
 from __future__ import annotations
 
+import ctypes
 import threading
 
 from . import _native
@@ -64,3 +69,35 @@ def rccl_group_comm(ctx, rank: int, world: int):
     else:
         dist.broadcast(buf, 0)
     return ctx.rccl_comm(bytes(buf.numpy().tobytes()), world, rank)
+
+
+def host_views(send: int, recv: int, send_bytes: int, recv_bytes: int):
+    """torch uint8 tensors viewing the library's pinned staging buffers (no copies)."""
+    import torch
+    sv = torch.frombuffer((ctypes.c_uint8 * send_bytes).from_address(send), dtype=torch.uint8) if send_bytes else \
+        torch.empty(0, dtype=torch.uint8)
+    rv = torch.frombuffer((ctypes.c_uint8 * recv_bytes).from_address(recv), dtype=torch.uint8) if recv_bytes else \
+        torch.empty(0, dtype=torch.uint8)
+    return sv, rv
+
+
+def gloo_transport(world: int, group=None):
+    """(all_to_all, all_gather) over torch.distributed on host memory (gloo)."""
+    import torch.distributed as dist
+
+    def all_to_all(send, recv, block):
+        sv, rv = host_views(send, recv, world * block, world * block)
+        if block:
+            dist.all_to_all_single(rv, sv, group=group)
+
+    def all_gather(send, recv, nbytes):
+        sv, rv = host_views(send, recv, nbytes, world * nbytes)
+        if nbytes:
+            dist.all_gather_into_tensor(rv, sv, group=group)
+    return all_to_all, all_gather
+
+
+def gloo_group_comm(rank: int, world: int, group=None):
+    """`zkp_comm` whose collectives run over torch.distributed (initialised with gloo)."""
+    a2a, ag = gloo_transport(world, group)
+    return _native.host_comm(rank, world, a2a, ag)
