@@ -1,0 +1,70 @@
+// NTT kernel timing harness (TUNING ONLY): builds with csrc/ntt.hip directly
+// (variant flags on the hipcc line) and times launch_ntt on the C2 shapes with
+// random canonical data. Prints ms per launch_ntt call and an output checksum,
+// which must agree across variants (all variants compute identical values).
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#include "../../zk_stark_project_amd/csrc/zkp_internal.hpp"
+
+// profiling stubs (the product's Prof lives in kernels.hip)
+hipEvent_t Prof::get_event() { return nullptr; }
+void Prof::begin(const char*, hipStream_t, double) {}
+void Prof::end(hipStream_t) {}
+
+static void fill(std::vector<felt>& v, uint64_t seed) {
+  for (auto& x : v) {
+    seed ^= seed << 13; seed ^= seed >> 7; seed ^= seed << 17;
+    uint64_t lo = seed;
+    seed ^= seed << 13; seed ^= seed >> 7; seed ^= seed << 17;
+    x.lo = lo;
+    x.hi = seed & 0x7fffffffffffffffull;  // < p
+  }
+}
+
+int main(int argc, char** argv) {
+  const uint32_t logn = argc > 1 ? atoi(argv[1]) : 20, logB = 3, logN = logn + logB;
+  const uint64_t n = 1ull << logn, N = 1ull << logN;
+  const uint32_t cols = 6, B = 1u << logB;
+  std::vector<felt> h_src((size_t)cols * n), h_tw(N), h_S((size_t)B * n);
+  fill(h_src, 1); fill(h_tw, 2); fill(h_S, 3);
+  felt *src, *dst, *tw, *S;
+  hipMalloc(&src, h_src.size() * 16); hipMalloc(&dst, (size_t)cols * N * 16);
+  hipMalloc(&tw, N * 16); hipMalloc(&S, h_S.size() * 16);
+  hipMemcpy(src, h_src.data(), h_src.size() * 16, hipMemcpyHostToDevice);
+  hipMemcpy(tw, h_tw.data(), N * 16, hipMemcpyHostToDevice);
+  hipMemcpy(S, h_S.data(), h_S.size() * 16, hipMemcpyHostToDevice);
+  hipStream_t st;
+  hipStreamCreate(&st);
+  Prof pf;
+  hipEvent_t e0, e1;
+  hipEventCreate(&e0); hipEventCreate(&e1);
+  auto run = [&](const char* name, auto fn, int iters) {
+    fn();
+    hipStreamSynchronize(st);
+    hipEventRecord(e0, st);
+    for (int i = 0; i < iters; i++) fn();
+    hipEventRecord(e1, st);
+    hipEventSynchronize(e1);
+    float ms;
+    hipEventElapsedTime(&ms, e0, e1);
+    std::vector<uint64_t> out((size_t)cols * N * 2);
+    hipMemcpy(out.data(), dst, out.size() * 8, hipMemcpyDeviceToHost);
+    uint64_t ck = 0;
+    for (size_t i = 0; i < out.size(); i++) ck = ck * 0x9e3779b97f4a7c15ull + out[i];
+    printf("%-34s %8.4f ms/call  checksum %016llx\n", name, ms / iters, (unsigned long long)ck);
+  };
+  // composition LDE: 6 columns x 8 cosets (DIT, coset scale fused)
+  NttBatch lde{src, dst, S, n, n, B, B, cols * B};
+  run("DIT lde 6 cols x 8 cosets", [&] { launch_ntt(pf, st, lde, logn, true, tw, logN); }, 10);
+  // trace LDE: 1 column x 8 cosets
+  NttBatch lde1{src, dst, S, n, n, B, B, B};
+  run("DIT lde 1 col x 8 cosets", [&] { launch_ntt(pf, st, lde1, logn, true, tw, logN); }, 20);
+  // CE-coset interpolation: 8 inverse transforms (DIF)
+  NttBatch inv8{src, dst, nullptr, n, n, 1, 1, 6};
+  run("DIF 6 arrays", [&] { launch_ntt(pf, st, inv8, logn, false, tw, logN); }, 20);
+  return 0;
+}

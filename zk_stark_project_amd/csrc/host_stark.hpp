@@ -120,6 +120,14 @@ struct Coin {
     }
     throw ZkpFail{ZKP_ERR_ARGUMENT, "failed to draw a field element"};
   }
+  // check_leading_zeros: trailing zeros of u64_le(merge_with_int(seed, nonce)[..8])
+  uint32_t leading_zeros(uint64_t nonce) const {
+    uint8_t v[32];
+    merge_with_int(seed, nonce, v);
+    uint64_t h = 0;
+    for (int b = 7; b >= 0; b--) h = (h << 8) | v[b];
+    return h == 0 ? 64u : (uint32_t)__builtin_ctzll(h);
+  }
   std::vector<uint64_t> draw_integers(uint32_t k, uint64_t domain, uint64_t nonce) {
     uint8_t s[32];
     merge_with_int(seed, nonce, s);

@@ -10,31 +10,12 @@
 //    cosets [j0, j0 + Bl) and stores them the same way with B -> Bl, j -> j - j0;
 //  * DEEP / FRI layer evaluations: coset-major too (coset j, position t);
 //  * Merkle trees: nodes[1..2L) of 8-word digests, leaves at nodes[L..2L).
-#include "../../include/zkp.h"
-#include "zkp_internal.hpp"
-#include "blake3.hpp"
+#include "kernels_common.hpp"
 
-#include <algorithm>
-#include <type_traits>
-
-using namespace fp;
-
-#define TPB 256
+using kc::rev_bits;
+using kc::static_for;
 
 namespace {
-
-__device__ __forceinline__ uint32_t rev_bits(uint32_t x, uint32_t bits) {
-  return bits == 0 ? 0u : (__brev(x) >> (32 - bits));
-}
-
-// compile-time unrolled loop: f(std::integral_constant<int, I>) for I in [B, E)
-template <int B, int E, typename F>
-__device__ __forceinline__ void static_for(F&& f) {
-  if constexpr (B < E) {
-    f(std::integral_constant<int, B>{});
-    static_for<B + 1, E>(f);
-  }
-}
 
 // w_N^e for e < N (table holds e < N/2; w_N^(N/2) = -1)
 __device__ __forceinline__ felt tw_full(const felt* tw, uint64_t e, uint32_t logN) {
@@ -61,395 +42,6 @@ __device__ __forceinline__ void load_digest(const uint32_t* src, uint32_t d[8]) 
   uint4 a = p[0], b = p[1];
   d[0] = a.x; d[1] = a.y; d[2] = a.z; d[3] = a.w;
   d[4] = b.x; d[5] = b.y; d[6] = b.z; d[7] = b.w;
-}
-
-// --------------------------------------------------------------------- NTT
-struct NttKArgs {
-  const felt* src;
-  felt* dst;
-  const felt* scale;
-  const felt* tw;
-  uint64_t src_stride, dst_stride;
-  uint32_t src_div, scale_mod;
-  uint32_t logn, s0, K, lo, T, Tl, logT, logTl, tw_shift, dit;
-};
-
-// One LDS pass of K radix-2 stages over T interleaved groups of 2^K elements.
-// Group g = (hi, l): elements hi*2^(lo+K) + q*2^lo + l, q < 2^K. Loads are
-// ordered so each wave reads runs of Tl (>= 8 when lo allows) contiguous felts.
-__global__ __launch_bounds__(TPB) void k_ntt_pass(NttKArgs a) {
-  extern __shared__ felt lds[];
-  const uint32_t bidx = blockIdx.y;
-  const felt* src = a.src + (uint64_t)(bidx / a.src_div) * a.src_stride;
-  felt* dst = a.dst + (uint64_t)bidx * a.dst_stride;
-  const felt* scale = a.scale ? a.scale + ((uint64_t)(bidx % a.scale_mod) << a.logn) : nullptr;
-  const uint32_t K = a.K, T = a.T, Tl = a.Tl, lo = a.lo;
-  const uint32_t E = T << K;
-  const uint64_t g0 = (uint64_t)blockIdx.x * T;
-  const uint64_t hi0 = g0 >> lo;
-  const uint64_t l0 = (Tl == T) ? (g0 & ((1ull << lo) - 1)) : 0;
-  const uint32_t qmask = (1u << K) - 1;
-
-  for (uint32_t e = threadIdx.x; e < E; e += TPB) {
-    uint32_t ll = e & (Tl - 1);
-    uint32_t rest = e >> a.logTl;
-    uint32_t q = rest & qmask;
-    uint32_t hl = rest >> K;
-    uint64_t addr = ((hi0 + hl) << (lo + K)) + ((uint64_t)q << lo) + l0 + ll;
-    felt v = src[addr];
-    if (scale) v = mul(v, scale[addr]);
-    lds[(q << a.logT) + (hl * Tl) + ll] = v;
-  }
-  __syncthreads();
-  for (uint32_t ls = 0; ls < K; ls++) {
-    const uint32_t s = a.s0 + ls;
-    const uint32_t pbit = a.dit ? ls : (K - 1 - ls);
-    const uint32_t lev = a.dit ? s : (a.logn - 1 - s);  // stage-major twiddle level
-    const felt* twl = a.tw + ((1ull << lev) - 1);
-    const uint32_t pmask = (1u << pbit) - 1;
-    for (uint32_t bf = threadIdx.x; bf < (E >> 1); bf += TPB) {
-      uint32_t gg = bf & (T - 1);
-      uint32_t qq = bf >> a.logT;
-      uint32_t q = ((qq >> pbit) << (pbit + 1)) | (qq & pmask);
-      uint32_t q2 = q | (1u << pbit);
-      uint64_t l = l0 + (gg & (Tl - 1));
-      uint64_t j = ((uint64_t)(q & pmask) << lo) | l;
-      felt w = twl[j];
-      uint32_t i0 = (q << a.logT) + gg, i1 = (q2 << a.logT) + gg;
-      felt x = lds[i0], y = lds[i1];
-      if (a.dit) {
-        felt t = mul(y, w);
-        lds[i0] = add(x, t);
-        lds[i1] = sub(x, t);
-      } else {
-        lds[i0] = add(x, y);
-        lds[i1] = mul(sub(x, y), w);
-      }
-    }
-    __syncthreads();
-  }
-  for (uint32_t e = threadIdx.x; e < E; e += TPB) {
-    uint32_t ll = e & (Tl - 1);
-    uint32_t rest = e >> a.logTl;
-    uint32_t q = rest & qmask;
-    uint32_t hl = rest >> K;
-    uint64_t addr = ((hi0 + hl) << (lo + K)) + ((uint64_t)q << lo) + l0 + ll;
-    dst[addr] = lds[(q << a.logT) + (hl * Tl) + ll];
-  }
-}
-
-// ------------------------------------------------------------- NTT radix-8
-// Register-blocked pass: each of NT threads owns 8 elements; a pass of K <= 10
-// stages runs as rounds of up to 3 stages (radix-8 / 2x radix-4 / 4x radix-2)
-// in registers with one LDS exchange per round. Global traffic is staged
-// through LDS in the coalesced (gg-fastest) order.
-struct Ntt8Args {
-  const felt* src;
-  felt* dst;
-  const felt* scale;
-  const felt* tw;
-  uint64_t src_stride, dst_stride;
-  uint32_t src_div, scale_mod;
-  uint32_t logn, s0, K, lo, logT, logTl, tw_shift, nrounds;
-  uint32_t rbits[4];
-};
-
-// stage-major twiddles: level t holds w_{2^(t+1)}^j at tw[(2^t - 1) + j]
-template <bool DIT>
-__device__ __forceinline__ felt ntt_tw(const Ntt8Args& a, uint64_t j, uint32_t pbit) {
-  uint32_t s = DIT ? a.s0 + pbit : a.s0 + a.K - 1 - pbit;
-  uint32_t lev = DIT ? s : a.logn - 1 - s;
-  return a.tw[((1ull << lev) - 1) + j];
-}
-
-template <bool DIT>
-__device__ __forceinline__ void bfly(felt& x, felt& y, felt w) {
-  if (DIT) {
-    felt t = mul(y, w);
-    y = sub(x, t);
-    x = add(x, t);
-  } else {
-    felt d = sub(x, y);
-    x = add(x, y);
-    y = mul(d, w);
-  }
-}
-
-#ifdef ZKP_EXP_NOBFLY
-#define ZKP_EXP_NOBFLY_ON true
-#else
-#define ZKP_EXP_NOBFLY_ON false
-#endif
-
-// butterfly with twiddle 1 (no product)
-template <bool DIT>
-__device__ __forceinline__ void bfly1(felt& x, felt& y) {
-  felt d = sub(x, y);
-  x = add(x, y);
-  y = d;
-}
-
-// rounds of a K-stage pass: <= 3 stages each, larger first
-template <int K>
-struct NttRounds {
-  static constexpr int n = (K + 2) / 3;
-  static constexpr int bits(int r) {
-    int rem = K;
-    for (int i = 0; i < r; i++) {
-      int left = n - i;
-      int b = (rem + left - 1) / left;
-      rem -= b > 3 ? 3 : b;
-    }
-    int left = n - r;
-    int b = (rem + left - 1) / left;
-    return b > 3 ? 3 : b;
-  }
-};
-
-// two independent butterflies with their products interleaved (fpd::mul_x2), so
-// each carry consumer sits two instructions after its producer
-template <bool DIT>
-__device__ __forceinline__ void bfly2(felt& x0, felt& y0, felt w0, felt& x1, felt& y1, felt w1) {
-#if defined(__HIP_DEVICE_COMPILE__)
-  if (DIT) {
-    felt t0, t1;
-    fpd::mul_x2(y0, w0, y1, w1, t0, t1);
-    y0 = sub(x0, t0); x0 = add(x0, t0);
-    y1 = sub(x1, t1); x1 = add(x1, t1);
-  } else {
-    felt d0 = sub(x0, y0), d1 = sub(x1, y1);
-    x0 = add(x0, y0); x1 = add(x1, y1);
-    fpd::mul_x2(d0, w0, d1, w1, y0, y1);
-  }
-#else
-  bfly<DIT>(x0, y0, w0);
-  bfly<DIT>(x1, y1, w1);
-#endif
-}
-
-// SMALL: this pass holds the transform's smallest stages 0..2 (DIT first pass /
-// DIF last pass, lo = 0); its round over them has jb = 0, so every twiddle of
-// stage 0, half of stage 1 and a quarter of stage 2 is 1 and those products are
-// skipped. A template flag, so the other passes keep their register budget.
-template <bool DIT, int NT, int KC, bool SMALL>
-__global__ __launch_bounds__(NT) void k_ntt8(Ntt8Args a) {
-  constexpr int E = NT * 8;
-  extern __shared__ felt lds[];
-  constexpr uint32_t K = KC;
-  constexpr uint32_t logT = 11 - KC;  // E = 2^11 elements per block
-  constexpr uint32_t T = 1u << logT;
-  const uint32_t Tl = 1u << a.logTl, lo = a.lo;
-  // LDS rows of T felts (T >= 8), XOR-swizzled by the row's low 3 bits: a wave's
-  // 8-lane groups then hit 8 distinct 16-B bank slots both when lanes walk a row
-  // (compute rounds) and when they walk down a column (staged loads, Tl = 1),
-  // with no padding: 2048 felts = 32 KB per block, 5 blocks per CU
-  auto lidx = [](uint32_t q, uint32_t x) -> uint32_t { return q * T + (x ^ (q & 7u)); };
-  // grid: x = batch (fastest in dispatch order), y = position block. The
-  // batches of one position block run back to back, dealt round-robin over the
-  // 8 XCDs: with B = 8 cosets batch b = col*B + j lands on XCD j, so the
-  // columns of a coset share its scale rows and every batch shares the pass's
-  // twiddles in that XCD's L2 instead of refetching them per array.
-  const uint32_t bidx = blockIdx.x;
-  const felt* src = a.src + (uint64_t)(bidx / a.src_div) * a.src_stride;
-  felt* dst = a.dst + (uint64_t)bidx * a.dst_stride;
-  const felt* scale = a.scale ? a.scale + ((uint64_t)(bidx % a.scale_mod) << a.logn) : nullptr;
-  const uint64_t g0 = (uint64_t)blockIdx.y << logT;
-  const uint64_t hi0 = g0 >> lo;
-  const uint64_t l0 = (Tl == T) ? (g0 & ((1ull << lo) - 1)) : 0;
-  const uint32_t qmask = (1u << K) - 1;
-  const uint32_t tid = threadIdx.x;
-  constexpr uint32_t LOGNT = NT == 1024 ? 10 : (NT == 512 ? 9 : 8);
-
-  // global address of block-local element (gg, q)
-  auto gaddr = [&](uint32_t gg, uint32_t q) -> uint64_t {
-    uint32_t hl = gg >> a.logTl, ll = gg & (Tl - 1);
-    return ((hi0 + hl) << (lo + K)) + ((uint64_t)q << lo) + l0 + ll;
-  };
-  (void)qmask;
-  // Passes whose groups have < 8 contiguous felts (lo < 3, e.g. the first DIT
-  // pass) would make every lane of a direct load/store touch its own 128-B
-  // line; those go through LDS in (ll, q, hl) order, contiguous along the wave.
-  const bool staged = a.logTl < 3;
-  auto staged_elem = [&](uint32_t e, uint32_t& slot) -> uint64_t {
-    uint32_t ll = e & (Tl - 1), rest = e >> a.logTl;
-    uint32_t q = rest & ((1u << K) - 1), hl = rest >> K;
-    slot = lidx(q, hl * Tl + ll);
-    return ((hi0 + hl) << (lo + K)) + ((uint64_t)q << lo) + l0 + ll;
-  };
-  if (staged) {
-#pragma unroll
-    for (int i = 0; i < 8; i++) {
-      uint32_t slot;
-      uint64_t ad = staged_elem(tid + i * NT, slot);
-#ifdef ZKP_EXP_NOGMEM
-      felt v = fp::make(ad, (uint64_t)i);
-      if (scale) v = mul(v, v);
-#else
-      felt v = src[ad];
-      if (scale) v = mul(v, scale[ad]);
-#endif
-      lds[slot] = v;
-    }
-    __syncthreads();
-  }
-  uint32_t b0 = DIT ? 0 : K;
-  static_for<0, NttRounds<KC>::n>([&](auto rr) {
-    constexpr int r = decltype(rr)::value;
-    constexpr uint32_t rb = NttRounds<KC>::bits(r);
-    if (!DIT) b0 -= rb;
-    constexpr bool first = r == 0, last = r + 1 == NttRounds<KC>::n;
-    if (!first) __syncthreads();
-    felt x[8];
-    uint32_t ggs[2], qlow[2];
-    // block-local coordinates (gg, q) of register m in this round
-    auto coord_gg = [&](int m) { return ((uint32_t)(m >> rb) << LOGNT | tid) & (T - 1); };
-    auto coord_q = [&](int m) {
-      uint32_t extra = m >> rb, bf = m & ((1u << rb) - 1);
-      uint32_t qo = ((extra << LOGNT) | tid) >> logT;
-      uint32_t ql = qo & ((1u << b0) - 1);
-      return ((qo >> b0) << (b0 + rb)) | (bf << b0) | ql;
-    };
-#pragma unroll
-    for (int m = 0; m < 8; m++) {
-      uint32_t extra = m >> rb, bf = m & ((1u << rb) - 1);
-      uint32_t c = (extra << LOGNT) | tid;
-      if (first && !staged) {  // straight from HBM (coalesced along gg), coset scale fused
-        uint64_t ad = gaddr(coord_gg(m), coord_q(m));
-#ifdef ZKP_EXP_NOGMEM  // timing experiment only (scripts/ntt_experiments.sh): no HBM reads
-        felt v = fp::make(ad, (uint64_t)m);
-        if (scale) v = mul(v, v);
-#else
-        felt v = src[ad];
-        if (scale) v = mul(v, scale[ad]);
-#endif
-        x[m] = v;
-      } else {
-        x[m] = lds[lidx(coord_q(m), coord_gg(m))];
-      }
-      if (bf == 0 && extra < 2) { ggs[extra] = c & (T - 1); qlow[extra] = (c >> logT) & ((1u << b0) - 1); }
-    }
-#ifdef ZKP_EXP_NOBFLY  // timing experiment only: data movement without butterflies
-    if constexpr (false) {
-#else
-    if constexpr (rb == 3) {
-#endif
-      const uint64_t l = l0 + (ggs[0] & (Tl - 1));
-      const uint64_t jb = ((uint64_t)qlow[0] << lo) | l;
-      const uint64_t jstep = 1ull << (b0 + lo);
-      // stages 0..2 (b0 = 0, lo = 0, so jb = 0): 7 of the 12 products are by 1
-      constexpr bool smallest = SMALL && (DIT ? first : last);
-      if constexpr (DIT && smallest) {
-        bfly1<true>(x[0], x[1]); bfly1<true>(x[2], x[3]); bfly1<true>(x[4], x[5]); bfly1<true>(x[6], x[7]);
-        const felt w1 = ntt_tw<true>(a, 1, 1);
-        bfly1<true>(x[0], x[2]); bfly1<true>(x[4], x[6]);
-        bfly2<true>(x[1], x[3], w1, x[5], x[7], w1);
-        const felt w21 = ntt_tw<true>(a, 1, 2), w22 = ntt_tw<true>(a, 2, 2), w23 = ntt_tw<true>(a, 3, 2);
-        bfly1<true>(x[0], x[4]);
-        bfly2<true>(x[1], x[5], w21, x[2], x[6], w22);
-        bfly<true>(x[3], x[7], w23);
-      } else if constexpr (!DIT && smallest) {
-        const felt w21 = ntt_tw<false>(a, 1, 2), w22 = ntt_tw<false>(a, 2, 2), w23 = ntt_tw<false>(a, 3, 2);
-        bfly1<false>(x[0], x[4]);
-        bfly2<false>(x[1], x[5], w21, x[2], x[6], w22);
-        bfly<false>(x[3], x[7], w23);
-        const felt w1 = ntt_tw<false>(a, 1, 1);
-        bfly1<false>(x[0], x[2]); bfly1<false>(x[4], x[6]);
-        bfly2<false>(x[1], x[3], w1, x[5], x[7], w1);
-        bfly1<false>(x[0], x[1]); bfly1<false>(x[2], x[3]); bfly1<false>(x[4], x[5]); bfly1<false>(x[6], x[7]);
-      } else if constexpr (DIT) {
-        {
-          felt w0 = ntt_tw<true>(a, jb, b0);
-          bfly2<true>(x[0], x[1], w0, x[2], x[3], w0); bfly2<true>(x[4], x[5], w0, x[6], x[7], w0);
-        }
-        {
-          felt w1a = ntt_tw<true>(a, jb, b0 + 1);
-          felt w1b = ntt_tw<true>(a, jb | jstep, b0 + 1);
-          bfly2<true>(x[0], x[2], w1a, x[1], x[3], w1b); bfly2<true>(x[4], x[6], w1a, x[5], x[7], w1b);
-        }
-        static_for<0, 2>([&](auto k2) {
-          felt w2a = ntt_tw<true>(a, jb | ((uint64_t)(2 * k2) << (b0 + lo)), b0 + 2);
-          felt w2b = ntt_tw<true>(a, jb | ((uint64_t)(2 * k2 + 1) << (b0 + lo)), b0 + 2);
-          bfly2<true>(x[2 * k2], x[2 * k2 + 4], w2a, x[2 * k2 + 1], x[2 * k2 + 5], w2b);
-        });
-      } else {
-        static_for<0, 2>([&](auto k2) {
-          felt w2a = ntt_tw<false>(a, jb | ((uint64_t)(2 * k2) << (b0 + lo)), b0 + 2);
-          felt w2b = ntt_tw<false>(a, jb | ((uint64_t)(2 * k2 + 1) << (b0 + lo)), b0 + 2);
-          bfly2<false>(x[2 * k2], x[2 * k2 + 4], w2a, x[2 * k2 + 1], x[2 * k2 + 5], w2b);
-        });
-        {
-          felt w1a = ntt_tw<false>(a, jb, b0 + 1);
-          felt w1b = ntt_tw<false>(a, jb | jstep, b0 + 1);
-          bfly2<false>(x[0], x[2], w1a, x[1], x[3], w1b); bfly2<false>(x[4], x[6], w1a, x[5], x[7], w1b);
-        }
-        {
-          felt w0 = ntt_tw<false>(a, jb, b0);
-          bfly2<false>(x[0], x[1], w0, x[2], x[3], w0); bfly2<false>(x[4], x[5], w0, x[6], x[7], w0);
-        }
-      }
-    } else if constexpr (rb == 2 && !ZKP_EXP_NOBFLY_ON) {
-      if constexpr (!DIT && SMALL && last) {  // DIF stages 1, 0: one product of four is not by 1
-        const felt w1 = ntt_tw<false>(a, 1, 1);
-#pragma unroll
-        for (int u = 0; u < 2; u++) {
-          felt* y = x + 4 * u;
-          bfly1<false>(y[0], y[2]);
-          bfly<false>(y[1], y[3], w1);
-          bfly1<false>(y[0], y[1]); bfly1<false>(y[2], y[3]);
-        }
-      } else {
-#pragma unroll
-      for (int u = 0; u < 2; u++) {
-        const uint64_t l = l0 + (ggs[u] & (Tl - 1));
-        const uint64_t jb = ((uint64_t)qlow[u] << lo) | l;
-        felt w0 = ntt_tw<DIT>(a, jb, b0);
-        felt w1a = ntt_tw<DIT>(a, jb, b0 + 1), w1b = ntt_tw<DIT>(a, jb | (1ull << (b0 + lo)), b0 + 1);
-        felt* y = x + 4 * u;
-        if (DIT) {
-          bfly2<true>(y[0], y[1], w0, y[2], y[3], w0);
-          bfly2<true>(y[0], y[2], w1a, y[1], y[3], w1b);
-        } else {
-          bfly2<false>(y[0], y[2], w1a, y[1], y[3], w1b);
-          bfly2<false>(y[0], y[1], w0, y[2], y[3], w0);
-        }
-      }
-      }
-    } else if constexpr (!ZKP_EXP_NOBFLY_ON) {
-#pragma unroll
-      for (int u = 0; u < 4; u++) {
-        uint32_t c = ((uint32_t)u << LOGNT) | tid;
-        uint32_t gg = c & (T - 1);
-        uint32_t ql = (c >> logT) & ((1u << b0) - 1);
-        const uint64_t jb = ((uint64_t)ql << lo) | (l0 + (gg & (Tl - 1)));
-        bfly<DIT>(x[2 * u], x[2 * u + 1], ntt_tw<DIT>(a, jb, b0));
-      }
-    }
-    if (!last || staged) __syncthreads();  // everyone has read this round's slots
-#pragma unroll
-    for (int m = 0; m < 8; m++) {
-#ifdef ZKP_EXP_NOGMEM
-      if (last && !staged && x[m].lo == 0x0123456789abcdefull) dst[gaddr(coord_gg(m), coord_q(m))] = x[m];
-#else
-      if (last && !staged) dst[gaddr(coord_gg(m), coord_q(m))] = x[m];  // straight to HBM
-#endif
-      else lds[lidx(coord_q(m), coord_gg(m))] = x[m];
-    }
-    if (DIT) b0 += rb;
-  });
-  if (staged) {  // LDS -> HBM in the contiguous order
-    __syncthreads();
-#pragma unroll
-    for (int i = 0; i < 8; i++) {
-      uint32_t slot;
-      uint64_t ad = staged_elem(tid + i * NT, slot);
-#ifdef ZKP_EXP_NOGMEM
-      if (lds[slot].lo == 0x0123456789abcdefull) dst[ad] = lds[slot];
-#else
-      dst[ad] = lds[slot];
-#endif
-    }
-  }
-  (void)E;
 }
 
 // ------------------------------------------------------------------ tables
@@ -1257,6 +849,107 @@ __global__ __launch_bounds__(TPB) void k_grind(SeedArg seed, const uint32_t* __r
   if (tz >= bits) atomicMin(result, (unsigned long long)nonce);
 }
 
+// Grinding to completion on the device: the minimum nonce >= base whose
+// BLAKE3(seed || nonce) has >= bits trailing zeros (seed = the device coin).
+// Thread g tests base + it*T + g in iteration it (T = all threads); it stops
+// once its iteration's first nonce exceeds a found nonce, so every smaller
+// candidate is still tested (minimum = sequential semantics) and every wave
+// exits (or at `limit`, leaving result untouched: the host reports no nonce).
+__global__ __launch_bounds__(TPB) void k_grind_all(const uint32_t* __restrict__ seedp, uint64_t base, uint64_t limit,
+                                                   uint32_t bits, unsigned long long* result) {
+  const uint64_t T = (uint64_t)gridDim.x * TPB, g = blockIdx.x * (uint64_t)TPB + threadIdx.x;
+  uint32_t sd[8];
+#pragma unroll
+  for (int k = 0; k < 8; k++) sd[k] = seedp[k];
+  for (uint64_t start = base;; start += T) {
+    if (start > limit || __hip_atomic_load(result, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < start) return;
+    const uint64_t nonce = start + g;
+    uint32_t m[16];
+#pragma unroll
+    for (int k = 0; k < 8; k++) m[k] = sd[k];
+    m[8] = (uint32_t)nonce;
+    m[9] = (uint32_t)(nonce >> 32);
+#pragma unroll
+    for (int k = 10; k < 16; k++) m[k] = 0;
+    uint32_t out[8];
+    b3::set_iv(out);
+    b3::compress(out, m, 0, 40, b3::CHUNK_START | b3::CHUNK_END | b3::ROOT);
+    const uint64_t h = (uint64_t)out[0] | ((uint64_t)out[1] << 32);
+    const uint32_t tz = h == 0 ? 64u : (uint32_t)__builtin_ctzll(h);
+    if (tz >= bits) atomicMin(result, (unsigned long long)nonce);
+  }
+}
+
+// DefaultRandomCoin::draw_integers(q, N, nonce) on the device coin: seed' =
+// merge_with_int(seed, nonce); position i = u64_le(merge_with_int(seed', i + 1)) & (N - 1).
+// Raw draws (unsorted, with repeats: the host sorts and dedups, as the prover does).
+__global__ void k_query_positions(const uint32_t* __restrict__ seedp, const unsigned long long* __restrict__ nonce_p,
+                                  uint32_t q, uint64_t N, uint64_t* __restrict__ pos) {
+  const uint64_t nonce = *nonce_p;
+  uint32_t m[16], s2[8];
+#pragma unroll
+  for (int k = 0; k < 8; k++) m[k] = seedp[k];
+  m[8] = (uint32_t)nonce;
+  m[9] = (uint32_t)(nonce >> 32);
+#pragma unroll
+  for (int k = 10; k < 16; k++) m[k] = 0;
+  b3::set_iv(s2);
+  b3::compress(s2, m, 0, 40, b3::CHUNK_START | b3::CHUNK_END | b3::ROOT);
+  for (uint32_t i = threadIdx.x; i < q; i += blockDim.x) {
+#pragma unroll
+    for (int k = 0; k < 8; k++) m[k] = s2[k];
+    m[8] = i + 1;
+    m[9] = 0;
+#pragma unroll
+    for (int k = 10; k < 16; k++) m[k] = 0;
+    uint32_t out[8];
+    b3::set_iv(out);
+    b3::compress(out, m, 0, 40, b3::CHUNK_START | b3::CHUNK_END | b3::ROOT);
+    pos[i] = ((uint64_t)out[0] | ((uint64_t)out[1] << 32)) & (N - 1);
+  }
+}
+
+// Every opening any batch proof over the drawn positions can need, gathered
+// without a host plan: for raw position i (block x) and segment y (0 = trace +
+// constraint rows, 1 + l = FRI layer l) the row values and the full sibling path
+// of the leaf (a batch proof's nodes are a subset of its leaves' sibling paths).
+// Layout per segment: q records of rec_words words at out + seg_off[y].
+__global__ __launch_bounds__(128) void k_gather_full(FullGatherArgs a, const uint64_t* __restrict__ pos,
+                                                     uint32_t* __restrict__ out) {
+  const uint32_t i = blockIdx.x, y = blockIdx.y, t = threadIdx.x;
+  const uint64_t p = pos[i];
+  const uint64_t B = 1ull << a.logB;
+  uint32_t* rec = out + a.seg_off[y] + (uint64_t)i * a.rec_words[y];
+  if (y == 0) {
+    const uint64_t j = p & (B - 1), tt = p >> a.logB;
+    const uint32_t nv = a.w + a.C, depth = a.logN;
+    for (uint32_t e = t; e < 4 * nv; e += blockDim.x) {  // row values: w trace then C constraint felts
+      const uint32_t c = e >> 2;
+      const felt* src = c < a.w ? a.tlde + ((uint64_t)c * B + j) * a.n : a.clde + ((uint64_t)(c - a.w) * B + j) * a.n;
+      rec[e] = reinterpret_cast<const uint32_t*>(src + tt)[e & 3];
+    }
+    uint32_t* paths = rec + 4 * nv;
+    for (uint32_t e = t; e < 2 * depth * 8; e += blockDim.x) {  // trace path, then constraint path
+      const uint32_t tree = e / (depth * 8), d = (e / 8) % depth, wd = e & 7;
+      const uint64_t node = (((1ull << a.logN) + p) >> d) ^ 1ull;
+      paths[e] = (tree ? a.cnodes : a.tnodes)[node * 8 + wd];
+    }
+  } else {
+    const uint32_t l = y - 1, logR = a.logrows[l];
+    const uint64_t r = p & ((1ull << logR) - 1), m = a.m[l];
+    for (uint32_t e = t; e < 64; e += blockDim.x) {  // 16 values E[r + k*Rows] (coset-major)
+      const uint64_t idx = r + ((uint64_t)(e >> 2) << logR);
+      const uint64_t j = idx & (B - 1), tt = idx >> a.logB;
+      rec[e] = reinterpret_cast<const uint32_t*>(a.E[l] + j * m + tt)[e & 3];
+    }
+    for (uint32_t e = t; e < logR * 8; e += blockDim.x) {
+      const uint32_t d = e / 8, wd = e & 7;
+      const uint64_t node = (((1ull << logR) + r) >> d) ^ 1ull;
+      rec[64 + e] = a.fnodes[l][node * 8 + wd];
+    }
+  }
+}
+
 // -------------------------------------------------------------- constraints
 constexpr int EVAL_CH = 8;  // points per thread (batch-inversion chunk)
 
@@ -1911,187 +1604,7 @@ void Prof::end(hipStream_t s) {
   open = false;
 }
 
-#define LAUNCH(prof, name, stream, bytes, ...)                 \
-  do {                                                          \
-    (prof).begin(name, stream, (double)(bytes));                \
-    __VA_ARGS__;                                                \
-    (prof).end(stream);                                         \
-  } while (0)
 
-std::vector<NttPass> ntt_plan(uint32_t logn, bool dit) {
-  const uint32_t KMAX = 8, LOGE = 12;
-  std::vector<NttPass> out;
-  if (logn == 0) return out;
-  uint32_t npass = (logn + KMAX - 1) / KMAX;
-  // pass sizes: prefer multiples of 3 (whole radix-8 rounds), largest pass last
-  uint32_t Ks[4] = {0, 0, 0, 0};
-  {
-    uint32_t rem = logn;
-    for (uint32_t p = 0; p < npass; p++) {
-      uint32_t left = npass - p;
-      uint32_t k = (rem + left - 1) / left;
-      if (left > 1) {
-        uint32_t k3 = k / 3 * 3;  // round down to whole radix-8 rounds if the rest still fits
-        if (k3 >= 3 && rem - k3 <= KMAX * (left - 1)) k = k3;
-      }
-      Ks[p] = k;
-      rem -= k;
-    }
-  }
-  uint32_t s0 = 0;
-  for (uint32_t p = 0; p < npass; p++) {
-    uint32_t K = Ks[p];
-    NttPass ps;
-    ps.logn = logn;
-    ps.s0 = s0;
-    ps.K = K;
-    ps.lo = dit ? s0 : logn - s0 - K;
-    uint32_t logG = logn - K;
-    uint32_t logT = LOGE - K < logG ? LOGE - K : logG;
-    uint32_t logTl = logT < ps.lo ? logT : ps.lo;
-    ps.T = 1u << logT;
-    ps.Tl = 1u << logTl;
-    out.push_back(ps);
-    s0 += K;
-  }
-  return out;
-}
-
-static void launch_ntt_radix2(Prof& prof, hipStream_t s, const NttBatch& b, uint32_t logn, bool dit,
-                              const felt* tw, uint32_t logN) {
-  auto plan = ntt_plan(logn, dit);
-  bool first = true;
-  for (const auto& ps : plan) {
-    NttKArgs a;
-    a.src = first ? b.src : b.dst;
-    a.dst = b.dst;
-    a.scale = first ? b.scale : nullptr;
-    a.tw = tw;
-    a.src_stride = first ? b.src_stride : b.dst_stride;
-    a.dst_stride = b.dst_stride;
-    a.src_div = first ? b.src_div : 1;
-    a.scale_mod = b.scale_mod ? b.scale_mod : 1;
-    a.logn = logn;
-    a.s0 = ps.s0;
-    a.K = ps.K;
-    a.lo = ps.lo;
-    a.T = ps.T;
-    a.Tl = ps.Tl;
-    a.logT = ilog2_u64(ps.T);
-    a.logTl = ilog2_u64(ps.Tl);
-    a.tw_shift = logN - logn;
-    a.dit = dit ? 1 : 0;
-    uint64_t groups = 1ull << (logn - ps.K);
-    dim3 grid((uint32_t)(groups / ps.T), b.batches);
-    size_t shmem = (size_t)(ps.T << ps.K) * sizeof(felt);
-    LAUNCH(prof, dit ? "ntt_dit_r2" : "ntt_dif_r2", s, (double)b.batches * (1ull << logn) * 16.0 * (a.scale ? 3 : 2),
-           hipLaunchKernelGGL(k_ntt_pass, grid, dim3(TPB), shmem, s, a));
-    first = false;
-  }
-}
-
-// radix-8 register-blocked passes: 256-thread blocks (E = 2048 elements, K <= 8)
-// for the big transforms (several blocks per CU overlap load and compute);
-// n must be >= 2^11.
-void launch_ntt(Prof& prof, hipStream_t s, const NttBatch& b, uint32_t logn, bool dit, const felt* tw,
-                uint32_t logN) {
-  const uint32_t LOGE = 11, KMAX = 8;
-  if (logn < LOGE) {
-    launch_ntt_radix2(prof, s, b, logn, dit, tw, logN);
-    return;
-  }
-  uint32_t npass = (logn + KMAX - 1) / KMAX;
-  static bool attr_set = false;
-  if (!attr_set) {
-    size_t maxb = (size_t)(1u << LOGE) * sizeof(felt);
-    const void* fns[] = {
-        (const void*)k_ntt8<true, 256, 5, false>,  (const void*)k_ntt8<true, 256, 6, false>,
-        (const void*)k_ntt8<true, 256, 7, false>,  (const void*)k_ntt8<true, 256, 8, false>,
-        (const void*)k_ntt8<false, 256, 5, false>, (const void*)k_ntt8<false, 256, 6, false>,
-        (const void*)k_ntt8<false, 256, 7, false>, (const void*)k_ntt8<false, 256, 8, false>,
-        (const void*)k_ntt8<true, 256, 5, true>,   (const void*)k_ntt8<true, 256, 6, true>,
-        (const void*)k_ntt8<true, 256, 7, true>,   (const void*)k_ntt8<true, 256, 8, true>,
-        (const void*)k_ntt8<false, 256, 5, true>,  (const void*)k_ntt8<false, 256, 6, true>,
-        (const void*)k_ntt8<false, 256, 7, true>,  (const void*)k_ntt8<false, 256, 8, true>};
-    for (const void* f : fns) (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)maxb);
-    attr_set = true;
-  }
-  // pass sizes: prefer multiples of 3 (whole radix-8 rounds), largest pass last
-  uint32_t Ks[4] = {0, 0, 0, 0};
-  {
-    uint32_t rem = logn;
-    for (uint32_t p = 0; p < npass; p++) {
-      uint32_t left = npass - p;
-      uint32_t k = (rem + left - 1) / left;
-      if (left > 1) {
-        uint32_t k3 = k / 3 * 3;  // round down to whole radix-8 rounds if the rest still fits
-        if (k3 >= 3 && rem - k3 <= KMAX * (left - 1)) k = k3;
-      }
-      Ks[p] = k;
-      rem -= k;
-    }
-  }
-  uint32_t s0 = 0;
-  for (uint32_t p = 0; p < npass; p++) {
-    uint32_t K = Ks[p];
-    Ntt8Args a;
-    bool first = p == 0;
-    a.src = first ? b.src : b.dst;
-    a.dst = b.dst;
-    a.scale = first ? b.scale : nullptr;
-    a.tw = tw;
-    a.src_stride = first ? b.src_stride : b.dst_stride;
-    a.dst_stride = b.dst_stride;
-    a.src_div = first ? b.src_div : 1;
-    a.scale_mod = b.scale_mod ? b.scale_mod : 1;
-    a.logn = logn;
-    a.s0 = s0;
-    a.K = K;
-    a.lo = dit ? s0 : logn - s0 - K;
-    a.logT = LOGE - K;
-    a.logTl = a.logT < a.lo ? a.logT : a.lo;
-    a.tw_shift = logN - logn;
-    // rounds of <= 3 bits, larger first
-    uint32_t nr = (K + 2) / 3, rem = K;
-    a.nrounds = nr;
-    for (uint32_t r = 0; r < 4; r++) a.rbits[r] = 0;
-    for (uint32_t r = 0; r < nr; r++) {
-      uint32_t rb = rem / (nr - r) + (rem % (nr - r) ? 1 : 0);
-      if (rb > 3) rb = 3;
-      a.rbits[r] = rb;
-      rem -= rb;
-    }
-    uint64_t groups = 1ull << (logn - K);
-    dim3 grid(b.batches, (uint32_t)(groups >> a.logT));  // batch fastest (see k_ntt8)
-    size_t shmem = (size_t)(1u << K) * (1u << a.logT) * sizeof(felt);
-    // compulsory bytes of this launch: every distinct input array once (the
-    // coefficient arrays are shared by src_div coset batches, the scale table
-    // has scale_mod rows) + every output once
-    const double arr = (double)(1ull << logn) * 16.0;
-    const uint32_t src_arrays = first ? (b.batches + a.src_div - 1) / a.src_div : b.batches;
-    const uint32_t scale_rows = a.scale ? (a.scale_mod < b.batches ? a.scale_mod : b.batches) : 0;
-    const double bytes = arr * ((double)src_arrays + scale_rows + b.batches);
-    // the pass over stages 0..2 (lo = 0): the trivial-twiddle variant
-    const bool small = a.lo == 0;
-#define ZKP_NTT8(D, KK)                                                                                  \
-  LAUNCH(prof, D ? "ntt_dit" : "ntt_dif", s, bytes,                                                     \
-         if (small) hipLaunchKernelGGL((k_ntt8<D, 256, KK, true>), grid, dim3(256), shmem, s, a);         \
-         else hipLaunchKernelGGL((k_ntt8<D, 256, KK, false>), grid, dim3(256), shmem, s, a))
-    switch (K * 2 + (dit ? 1 : 0)) {
-      case 11: ZKP_NTT8(true, 5); break;
-      case 13: ZKP_NTT8(true, 6); break;
-      case 15: ZKP_NTT8(true, 7); break;
-      case 17: ZKP_NTT8(true, 8); break;
-      case 10: ZKP_NTT8(false, 5); break;
-      case 12: ZKP_NTT8(false, 6); break;
-      case 14: ZKP_NTT8(false, 7); break;
-      case 16: ZKP_NTT8(false, 8); break;
-      default: abort();  // launch_ntt only plans passes of 5..8 stages
-    }
-#undef ZKP_NTT8
-    s0 += K;
-  }
-}
 
 void launch_build_levels(Prof& prof, hipStream_t s, felt* tab, uint32_t top) {
   LAUNCH(prof, "build_levels", s, (double)(1ull << top) * 32.0,
@@ -2222,6 +1735,24 @@ void launch_grind(Prof& prof, hipStream_t s, const uint32_t* seed_words, const u
   LAUNCH(prof, "grind", s, 0.0,
          hipLaunchKernelGGL(k_grind, dim3(blocks_for(count)), dim3(TPB), 0, s, sa, seed_dev, base, count, bits,
                             result));
+}
+
+void launch_grind_all(Prof& prof, hipStream_t s, const uint32_t* seed_dev, uint64_t base, uint64_t limit,
+                      uint32_t bits, unsigned long long* result) {
+  LAUNCH(prof, "grind", s, 0.0,
+         hipLaunchKernelGGL(k_grind_all, dim3(4096), dim3(TPB), 0, s, seed_dev, base, limit, bits, result));
+}
+
+void launch_query_positions(Prof& prof, hipStream_t s, const uint32_t* seed_dev, const unsigned long long* nonce,
+                            uint32_t q, uint64_t N, uint64_t* pos) {
+  LAUNCH(prof, "positions", s, 0.0, hipLaunchKernelGGL(k_query_positions, dim3(1), dim3(256), 0, s, seed_dev, nonce, q,
+                                                       N, pos));
+}
+
+void launch_gather_full(Prof& prof, hipStream_t s, const FullGatherArgs& a, uint32_t q, const uint64_t* pos,
+                        uint32_t* out) {
+  LAUNCH(prof, "gather", s, 0.0,
+         hipLaunchKernelGGL(k_gather_full, dim3(q, 1 + a.nlayers), dim3(128), 0, s, a, pos, out));
 }
 
 void launch_pack(Prof& prof, hipStream_t s, const PackArgs& a, void* dst) {

@@ -1,0 +1,43 @@
+// kernels_common.hpp — helpers shared by the kernel translation units
+// (kernels.hip, ntt.hip): launch accounting, compile-time loops, domain points.
+#pragma once
+#include "../../include/zkp.h"
+#include "zkp_internal.hpp"
+#include "blake3.hpp"
+
+#include <algorithm>
+#include <type_traits>
+
+using namespace fp;
+
+#define TPB 256
+
+#define LAUNCH(prof, name, stream, bytes, ...)                 \
+  do {                                                          \
+    (prof).begin(name, stream, (double)(bytes));                \
+    __VA_ARGS__;                                                \
+    (prof).end(stream);                                         \
+  } while (0)
+
+namespace kc {
+
+__device__ __forceinline__ uint32_t rev_bits(uint32_t x, uint32_t bits) {
+  return bits == 0 ? 0u : (__brev(x) >> (32 - bits));
+}
+
+// compile-time unrolled loop: f(std::integral_constant<int, I>) for I in [B, E)
+template <int B, int E, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (B < E) {
+    f(std::integral_constant<int, B>{});
+    static_for<B + 1, E>(f);
+  }
+}
+
+inline uint32_t ilog2_u64(uint64_t v) {
+  uint32_t l = 0;
+  while ((1ull << l) < v) l++;
+  return l;
+}
+
+}  // namespace kc

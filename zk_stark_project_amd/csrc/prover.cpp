@@ -740,6 +740,94 @@ void gather_openings(zkp_ctx* ctx, zkp_comm* cm, const std::vector<uint64_t>& po
   }
 }
 
+// Openings assembled on the host from the device's full gather (k_gather_full,
+// world 1): the row values of every drawn position and the full sibling path of
+// every leaf; the batch plans (plan_batch) pick their nodes from those paths.
+// `raw` = the drawn positions in draw order (the gather's record order), `pos`
+// = sorted unique; the result has gather_openings' segment layout.
+void openings_from_full(const std::vector<uint64_t>& raw, const std::vector<uint64_t>& pos, const uint32_t* full,
+                        const FullGatherArgs& ga, const std::vector<FriLayer>& layers, uint32_t L, uint32_t F,
+                        Openings& op) {
+  const uint32_t w = ga.w, C = ga.C, nv = w + C, logN = ga.logN;
+  const uint64_t N = 1ull << logN, B = 1ull << ga.logB;
+  auto missing = [] { return ZkpFail{ZKP_ERR_DEVICE, "device query gather is missing an opening"}; };
+  // (leaf node index L + row, record index) sorted by node: node k at height d is on
+  // the path of the leaves whose node index lies in [k << d, (k + 1) << d)
+  struct Leaves {
+    std::vector<std::pair<uint64_t, uint32_t>> v;
+    uint32_t logL;
+    // record of any drawn leaf below node k (height d above the leaves); -1 if none
+    int64_t below(uint64_t k, uint32_t d) const {
+      auto it = std::lower_bound(v.begin(), v.end(), std::make_pair(k << d, 0u));
+      return it != v.end() && (it->first >> d) == k ? (int64_t)it->second : -1;
+    }
+    // height of node k above the leaves
+    uint32_t height(uint64_t k) const { return logL - (63 - __builtin_clzll(k)); }
+  };
+  auto leaves_of = [&](uint64_t Lcount, uint32_t logL) {
+    Leaves lv;
+    lv.logL = logL;
+    lv.v.reserve(raw.size());
+    for (size_t i = 0; i < raw.size(); i++) lv.v.push_back({Lcount + (raw[i] & (Lcount - 1)), (uint32_t)i});
+    std::sort(lv.v.begin(), lv.v.end());
+    return lv;
+  };
+  op.segs.clear();
+  op.gathered.clear();
+  op.gathered.reserve(full ? 4096 : 0);
+  auto begin_seg = [&](uint32_t words) {
+    GatherSeg g{};
+    g.out_off = op.gathered.size();
+    g.words = words;
+    op.segs.push_back(g);
+  };
+  auto put = [&](const uint32_t* src, uint32_t words) {
+    op.gathered.insert(op.gathered.end(), src, src + words);
+    op.segs.back().count++;
+  };
+  // a batch path node k is the sibling, at height d, of a drawn leaf's path: the record
+  // of a leaf below k ^ 1 holds it at path slot d
+  auto paths = [&](const BatchPlan& bp, const Leaves& lv, uint32_t seg, uint32_t path_off) {
+    begin_seg(8);
+    for (auto& pth : bp.paths)
+      for (uint64_t k : pth) {
+        const uint32_t d = lv.height(k);
+        const int64_t i = lv.below(k ^ 1ull, d);
+        if (i < 0) throw missing();
+        put(full + ga.seg_off[seg] + (uint64_t)i * ga.rec_words[seg] + path_off + 8 * d, 8);
+      }
+  };
+  const Leaves l0 = leaves_of(N, logN);
+  op.bt = plan_batch(N, pos);
+  for (int seg = 0; seg < 2; seg++) {  // values, then batch paths, of the trace and constraint commitments
+    begin_seg(4);
+    for (uint64_t p : pos) {
+      const int64_t i = l0.below(N + p, 0);
+      if (i < 0) throw missing();
+      const uint32_t* r = full + (uint64_t)i * ga.rec_words[0];
+      for (uint32_t c = seg ? w : 0; c < (seg ? nv : w); c++) put(r + 4 * c, 4);
+    }
+    paths(op.bt, l0, 0, 4 * nv + (seg ? 8 * logN : 0));
+  }
+  op.bf.assign(L, BatchPlan{});
+  std::vector<uint64_t> cur = pos;
+  for (uint32_t l = 0; l < L; l++) {
+    const uint64_t Rows = B * (layers[l].m / F);
+    const Leaves lv = leaves_of(Rows, ga.logrows[l]);
+    std::vector<uint64_t> fp = fold_positions(cur, Rows);
+    op.bf[l] = plan_batch(Rows, fp);
+    begin_seg(4);
+    for (uint64_t r : fp) {
+      const int64_t i = lv.below(Rows + r, 0);
+      if (i < 0) throw missing();
+      const uint32_t* rec = full + ga.seg_off[1 + l] + (uint64_t)i * ga.rec_words[1 + l];
+      for (uint32_t k = 0; k < F; k++) put(rec + 4 * k, 4);
+    }
+    paths(op.bf[l], lv, 1 + l, 64);
+    cur = fp;
+  }
+}
+
 // constants of the fold-16 iDFT (w_16^-m for m < 8, then 16^-1), cached per context
 const felt* fold_constants(zkp_ctx* ctx) {
   felt* deps = ctx->buf<felt>("eps_inv", 9);
@@ -982,6 +1070,12 @@ int prove_impl(zkp_ctx* ctx, zkp_comm* cm, int air_id, const felt* d_trace, uint
   std::vector<FriLayer> layers(L + 1);
   std::vector<felt> remainder;
   bool dev_tail = false;  // remainder + first grinding chunk on the device
+  bool dev_query = false;  // ... and the whole query tail (world 1)
+  FullGatherArgs ga{};
+  uint64_t* dpos = nullptr;
+  const uint32_t* full_d = nullptr;
+  std::vector<uint32_t> full_h;
+  std::vector<uint64_t> raw_pos;
   felt* rem_d = nullptr;
   uint32_t* rcommit_d = nullptr;
   unsigned long long* dres = ctx->buf<unsigned long long>("grind_res", 1);
@@ -1050,13 +1144,44 @@ int prove_impl(zkp_ctx* ctx, zkp_comm* cm, int air_id, const felt* d_trace, uint
     // returns the nonce (the host replays and checks all of it)
     const uint64_t Dlast = (uint64_t)B * m;
     dev_tail = Dlast <= 256 && o->grinding_factor > 0;
+    // world 1: the whole query tail runs on the device too (grinding to completion,
+    // query positions, every opening the batch proofs can need), so the proof has
+    // a single host round trip, at its end
+    dev_query = dev_tail && R == 1 && L <= GATHER_MAX_LAYERS;
     if (dev_tail) {
       rem_d = ctx->buf<felt>("rem_d", m + 1);
       rcommit_d = ctx->buf<uint32_t>("rem_commit", 8);
       launch_fri_remainder(pf, st, E, logB, (uint32_t)m, inv(off), inv(root_of_unity(ilog2(Dlast))),
                            inv(felt_u64(Dlast)), coin_d, rem_d, rcommit_d);
       HIP_CHECK(hipMemsetAsync(dres, 0xff, 8, st));
-      launch_grind(pf, st, nullptr, coin_d, 1, grind_chunk, o->grinding_factor, dres);
+      if (dev_query)
+        launch_grind_all(pf, st, coin_d, 1, 1ull << 40, o->grinding_factor, dres);
+      else
+        launch_grind(pf, st, nullptr, coin_d, 1, grind_chunk, o->grinding_factor, dres);
+    }
+    if (dev_query) {
+      dpos = ctx->buf<uint64_t>("query_pos", o->num_queries);
+      launch_query_positions(pf, st, coin_d, dres, o->num_queries, N, dpos);
+      ga.tlde = tlde; ga.clde = clde; ga.tnodes = ttree.nodes; ga.cnodes = ctree.nodes;
+      ga.n = n; ga.w = w; ga.C = C; ga.logB = logB; ga.logN = logN; ga.nlayers = L;
+      uint64_t off_w = 0;
+      ga.seg_off[0] = 0;
+      ga.rec_words[0] = 4 * (w + C) + 16 * logN;
+      off_w += (uint64_t)o->num_queries * ga.rec_words[0];
+      for (uint32_t l = 0; l < L; l++) {
+        ga.E[l] = layers[l].E;
+        ga.fnodes[l] = layers[l].tree.nodes;
+        ga.m[l] = layers[l].m;
+        ga.logrows[l] = logB + ilog2(layers[l].m / F);
+        ga.seg_off[1 + l] = off_w;
+        ga.rec_words[1 + l] = 64 + 8 * ga.logrows[l];
+        off_w += (uint64_t)o->num_queries * ga.rec_words[1 + l];
+      }
+      full_h.resize(off_w);
+      uint32_t* dfull = ctx->buf<uint32_t>("query_full", off_w + 4);
+      launch_gather_full(pf, st, ga, o->num_queries, dpos, dfull);
+      raw_pos.resize(o->num_queries);
+      full_d = dfull;
     }
     // the proof's first host round trip: the device transcript so far (commitment
     // roots, coefficients, z, OOD frame, DEEP coefficients, FRI roots + alphas)
@@ -1077,6 +1202,10 @@ int prove_impl(zkp_ctx* ctx, zkp_comm* cm, int air_id, const felt* d_trace, uint
       fs.push_back({drcommit, rcommit_d, 32});
       fs.push_back({dseed, coin_d, 32});
       fs.push_back({&dnonce, dres, 8});
+    }
+    if (dev_query) {
+      fs.push_back({raw_pos.data(), dpos, raw_pos.size() * 8});
+      fs.push_back({full_h.data(), full_d, full_h.size() * 4});
     }
     fetch_all(ctx, fs);
     memcpy(T.trace_root, roots, 32);
@@ -1147,6 +1276,9 @@ int prove_impl(zkp_ctx* ctx, zkp_comm* cm, int air_id, const felt* d_trace, uint
     if (dev_tail) {  // the first chunk ran on the device seed (checked equal to coin.seed above)
       if (dnonce != ~0ull) nonce = dnonce;
       base0 = 1 + chunk;
+      if (dev_query && nonce == 0) throw ZkpFail{ZKP_ERR_NONCE, "nonce not found"};
+      if (dev_query && coin.leading_zeros(nonce) < o->grinding_factor)
+        throw ZkpFail{ZKP_ERR_DEVICE, "device grinding nonce fails the host check"};
     }
     for (uint64_t base = base0; nonce == 0; base += chunk) {
       unsigned long long init = ~0ull;
@@ -1163,6 +1295,7 @@ int prove_impl(zkp_ctx* ctx, zkp_comm* cm, int air_id, const felt* d_trace, uint
 
   // 9. query positions
   std::vector<uint64_t> pos = coin.draw_integers(o->num_queries, N, nonce);
+  if (dev_query && pos != raw_pos) throw ZkpFail{ZKP_ERR_DEVICE, "device query positions diverged from the host"};
   std::sort(pos.begin(), pos.end());
   pos.erase(std::unique(pos.begin(), pos.end()), pos.end());
   const uint64_t np = pos.size();
@@ -1171,7 +1304,10 @@ int prove_impl(zkp_ctx* ctx, zkp_comm* cm, int air_id, const felt* d_trace, uint
   T.num_composition_columns = C;
 
   Openings op;
-  gather_openings(ctx, cm, pos, n, logB, j0, tlde, w, ttree, clde, C, ctree, layers, L, F, op);
+  if (dev_query)
+    openings_from_full(raw_pos, pos, full_h.data(), ga, layers, L, F, op);
+  else
+    gather_openings(ctx, cm, pos, n, logB, j0, tlde, w, ttree, clde, C, ctree, layers, L, F, op);
   const uint64_t out_words = op.gathered.size();
   // 10. serialize (≙ Proof::to_bytes)
   Writer wr;

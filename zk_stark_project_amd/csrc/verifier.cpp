@@ -327,12 +327,7 @@ int verify_impl(int air_id, const uint8_t* proof, uint64_t len, const zkp_felt* 
 
   // ---- 4. proof of work + query positions
   {
-    uint8_t v[32];
-    merge_with_int(coin.seed, nonce, v);
-    uint64_t h = 0;
-    for (int b = 7; b >= 0; b--) h = (h << 8) | v[b];
-    uint32_t tz = h == 0 ? 64u : (uint32_t)__builtin_ctzll(h);
-    if (tz < o.grinding_factor) return ZKP_VERIFY_POW;
+    if (coin.leading_zeros(nonce) < o.grinding_factor) return ZKP_VERIFY_POW;
   }
   std::vector<uint64_t> pos = coin.draw_integers(o.num_queries, N, nonce);
   std::sort(pos.begin(), pos.end());

@@ -118,6 +118,33 @@ void launch_grind(Prof& prof, hipStream_t s, const uint32_t* seed_words, const u
 void launch_fri_remainder(Prof& prof, hipStream_t s, const felt* E, uint32_t logB, uint32_t m, felt off_inv,
                           felt wd_inv, felt d_inv, uint32_t* seed, felt* rem_out, uint32_t* commit_out);
 
+// ---- device query tail (world 1): grinding to completion, query positions,
+// and every opening of every possible batch proof (rows + full sibling paths)
+void launch_grind_all(Prof& prof, hipStream_t s, const uint32_t* seed_dev, uint64_t base, uint64_t limit,
+                      uint32_t bits, unsigned long long* result);
+// raw DefaultRandomCoin::draw_integers(q, N, *nonce) from the device coin state
+void launch_query_positions(Prof& prof, hipStream_t s, const uint32_t* seed_dev, const unsigned long long* nonce,
+                            uint32_t q, uint64_t N, uint64_t* pos);
+constexpr uint32_t GATHER_MAX_LAYERS = 16;
+struct FullGatherArgs {
+  const felt* tlde;      // w x B x n (coset-major)
+  const felt* clde;      // C x B x n
+  const uint32_t* tnodes;
+  const uint32_t* cnodes;
+  uint64_t n;
+  uint32_t w, C, logB, logN, nlayers;
+  const felt* E[GATHER_MAX_LAYERS];         // FRI layer l evaluations, coset-major (m[l] per coset)
+  const uint32_t* fnodes[GATHER_MAX_LAYERS];
+  uint64_t m[GATHER_MAX_LAYERS];
+  uint32_t logrows[GATHER_MAX_LAYERS];      // log2 of the layer's tree leaves (rows)
+  uint64_t seg_off[GATHER_MAX_LAYERS + 1];  // words
+  uint32_t rec_words[GATHER_MAX_LAYERS + 1];
+};
+// record of raw position i in segment 0: [w + C row felts | trace path | constraint path]
+// (logN sibling digests each, leaf level first); segment 1 + l: [16 felts | logrows[l] digests]
+void launch_gather_full(Prof& prof, hipStream_t s, const FullGatherArgs& a, uint32_t q, const uint64_t* pos,
+                        uint32_t* out);
+
 // ---------------------------------------------------------------- device transcript
 // (seed = 8 LE words of the DefaultRandomCoin state, in device memory)
 // reseed with `root` (device), then draw `ncoef` composition coefficients into cc
