@@ -15,6 +15,11 @@ hipEvent_t Prof::get_event() { return nullptr; }
 void Prof::begin(const char*, hipStream_t, double) {}
 void Prof::end(hipStream_t) {}
 
+__global__ void k_copy(const uint4* __restrict__ a, uint4* __restrict__ b, uint64_t n) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    b[i] = a[i];
+}
+
 static void fill(std::vector<felt>& v, uint64_t seed) {
   for (auto& x : v) {
     seed ^= seed << 13; seed ^= seed >> 7; seed ^= seed << 17;
@@ -57,6 +62,24 @@ int main(int argc, char** argv) {
     for (size_t i = 0; i < out.size(); i++) ck = ck * 0x9e3779b97f4a7c15ull + out[i];
     printf("%-34s %8.4f ms/call  checksum %016llx\n", name, ms / iters, (unsigned long long)ck);
   };
+  {
+    felt* big;
+    hipMalloc(&big, (size_t)cols * N * 16);
+    const uint64_t nv = (uint64_t)cols * N;  // 16-B elements
+    hipEvent_t c0, c1;
+    hipEventCreate(&c0); hipEventCreate(&c1);
+    hipLaunchKernelGGL(k_copy, dim3(8192), dim3(256), 0, st, (const uint4*)dst, (uint4*)big, nv);
+    hipEventRecord(c0, st);
+    for (int i = 0; i < 10; i++)
+      hipLaunchKernelGGL(k_copy, dim3(8192), dim3(256), 0, st, (const uint4*)dst, (uint4*)big, nv);
+    hipEventRecord(c1, st);
+    hipEventSynchronize(c1);
+    float ms;
+    hipEventElapsedTime(&ms, c0, c1);
+    printf("%-34s %8.4f ms/call  %.2f TB/s (read+write)\n", "copy 6 x 8 x n felts", ms / 10,
+           2.0 * nv * 16 / (ms / 10 * 1e-3) / 1e12);
+    hipFree(big);
+  }
   // composition LDE: 6 columns x 8 cosets (DIT, coset scale fused)
   NttBatch lde{src, dst, S, n, n, B, B, cols * B};
   run("DIT lde 6 cols x 8 cosets", [&] { launch_ntt(pf, st, lde, logn, true, tw, logN); }, 10);

@@ -15,7 +15,8 @@ import numpy as np
 from .options import ProofOptions
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libzkp.so")
+# ZKP_LIB: an alternative build of the same library (A/B timing of kernel variants)
+LIB_PATH = os.environ.get("ZKP_LIB") or os.path.join(HERE, "libzkp.so")
 
 ZKP_OK = 0
 STATUS = {

@@ -1651,8 +1651,10 @@ bool merkle_upper(Prof& prof, hipStream_t s, uint32_t* nodes, uint64_t L, const 
     // per lane); below that the 9-level LDS-fused blocks have the shorter
     // critical path (9 merges) and fill more CUs
     if (L >= (1ull << 18)) {
-      merkle_pass<2>(prof, s, a, 4, "merkle_upper", (double)L * 32.0 * 1.5);
-      L >>= 4;
+      // 2 levels per lane: measured faster than 3-4 (fewer live digests, more waves;
+      // tests/native/kbench_merkle.cpp, profiles/r02_kbench_merkle.txt)
+      merkle_pass<2>(prof, s, a, 2, "merkle_upper", (double)L * 32.0 * 1.5);
+      L >>= 2;
     } else {
       uint64_t blocks = (L + 511) / 512;
       const bool finish = tail && tail->done && blocks <= 512;  // this launch completes the tree
@@ -1675,8 +1677,9 @@ bool launch_merkle_lde(Prof& prof, hipStream_t s, const felt* lde, uint32_t cols
   a.logB = logB;
   a.nodes = nodes;
   a.L = L;
-  uint32_t H = 0;
-  while (H < 3 && (1ull << (H + 1)) <= L) H++;
+  // each lane hashes 2 rows and merges them (H = 1): measured faster than deeper
+  // lane subtrees, whose extra live digests cost waves (kbench_merkle.cpp)
+  const uint32_t H = L >= 2 ? 1 : 0;
   merkle_pass<0>(prof, s, a, H, "merkle_lde", (double)L * (cols * 16.0 + 64.0));
   return merkle_upper(prof, s, nodes, L >> H, tail);
 }

@@ -3,6 +3,9 @@
 // kernels.hip so the hottest kernel rebuilds on its own.
 #include "kernels_common.hpp"
 
+#include <algorithm>
+#include <cstdlib>
+
 using kc::static_for;
 using kc::rev_bits;
 
@@ -181,8 +184,10 @@ __global__ __launch_bounds__(NT) void k_ntt8(Ntt8Args a) {
   constexpr int E = NT * 8;
   extern __shared__ felt lds[];
   constexpr uint32_t K = KC;
-  constexpr uint32_t logT = 11 - KC;  // E = 2^11 elements per block
+  constexpr uint32_t LOGNT = NT == 1024 ? 10 : (NT == 512 ? 9 : 8);
+  constexpr uint32_t logT = LOGNT + 3 - KC;  // E = NT * 8 elements per block
   constexpr uint32_t T = 1u << logT;
+  static_assert(T >= 8, "the LDS swizzle needs rows of >= 8 felts");
   const uint32_t Tl = 1u << a.logTl, lo = a.lo;
   // LDS rows of T felts (T >= 8), XOR-swizzled by the row's low 3 bits: a wave's
   // 8-lane groups then hit 8 distinct 16-B bank slots both when lanes walk a row
@@ -194,16 +199,23 @@ __global__ __launch_bounds__(NT) void k_ntt8(Ntt8Args a) {
   // 8 XCDs: with B = 8 cosets batch b = col*B + j lands on XCD j, so the
   // columns of a coset share its scale rows and every batch shares the pass's
   // twiddles in that XCD's L2 instead of refetching them per array.
+#ifdef ZKP_NTT_POSFAST
+  const uint32_t bidx = blockIdx.y;  // position blocks fastest in dispatch order
+#else
   const uint32_t bidx = blockIdx.x;
+#endif
   const felt* src = a.src + (uint64_t)(bidx / a.src_div) * a.src_stride;
   felt* dst = a.dst + (uint64_t)bidx * a.dst_stride;
   const felt* scale = a.scale ? a.scale + ((uint64_t)(bidx % a.scale_mod) << a.logn) : nullptr;
+#ifdef ZKP_NTT_POSFAST
+  const uint64_t g0 = (uint64_t)blockIdx.x << logT;
+#else
   const uint64_t g0 = (uint64_t)blockIdx.y << logT;
+#endif
   const uint64_t hi0 = g0 >> lo;
   const uint64_t l0 = (Tl == T) ? (g0 & ((1ull << lo) - 1)) : 0;
   const uint32_t qmask = (1u << K) - 1;
   const uint32_t tid = threadIdx.x;
-  constexpr uint32_t LOGNT = NT == 1024 ? 10 : (NT == 512 ? 9 : 8);
 
   // global address of block-local element (gg, q)
   auto gaddr = [&](uint32_t gg, uint32_t q) -> uint64_t {
@@ -476,7 +488,15 @@ static void launch_ntt_radix2(Prof& prof, hipStream_t s, const NttBatch& b, uint
 // n must be >= 2^11.
 void launch_ntt(Prof& prof, hipStream_t s, const NttBatch& b, uint32_t logn, bool dit, const felt* tw,
                 uint32_t logN) {
-  const uint32_t LOGE = 11, KMAX = 8;
+  const uint32_t LOGE = 11;
+#ifndef ZKP_NTT_KMAX
+#define ZKP_NTT_KMAX 8
+#endif
+  // passes of up to KMAX stages; passes of 9-10 stages run 1024-thread blocks of
+  // 8192 elements (128 KB LDS), so their strided groups still load 8-felt runs
+  // (ZKP_NTT_KMAX=10 builds the 2-pass 2^20 schedule: measured slower, one
+  // 128-KB block per CU cannot overlap its loads with compute)
+  const uint32_t KMAX = logn >= 18 ? ZKP_NTT_KMAX : 8;
   if (logn < LOGE) {
     launch_ntt_radix2(prof, s, b, logn, dit, tw, logN);
     return;
@@ -484,7 +504,7 @@ void launch_ntt(Prof& prof, hipStream_t s, const NttBatch& b, uint32_t logn, boo
   uint32_t npass = (logn + KMAX - 1) / KMAX;
   static bool attr_set = false;
   if (!attr_set) {
-    size_t maxb = (size_t)(1u << LOGE) * sizeof(felt);
+    size_t maxb = (size_t)(1u << LOGE) * sizeof(felt), bigb = (size_t)(1u << 13) * sizeof(felt);
     const void* fns[] = {
         (const void*)k_ntt8<true, 256, 5, false>,  (const void*)k_ntt8<true, 256, 6, false>,
         (const void*)k_ntt8<true, 256, 7, false>,  (const void*)k_ntt8<true, 256, 8, false>,
@@ -495,6 +515,14 @@ void launch_ntt(Prof& prof, hipStream_t s, const NttBatch& b, uint32_t logn, boo
         (const void*)k_ntt8<false, 256, 5, true>,  (const void*)k_ntt8<false, 256, 6, true>,
         (const void*)k_ntt8<false, 256, 7, true>,  (const void*)k_ntt8<false, 256, 8, true>};
     for (const void* f : fns) (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)maxb);
+#if ZKP_NTT_KMAX > 8
+    const void* big[] = {
+        (const void*)k_ntt8<true, 1024, 9, false>,  (const void*)k_ntt8<true, 1024, 10, false>,
+        (const void*)k_ntt8<false, 1024, 9, false>, (const void*)k_ntt8<false, 1024, 10, false>,
+        (const void*)k_ntt8<true, 1024, 9, true>,   (const void*)k_ntt8<true, 1024, 10, true>,
+        (const void*)k_ntt8<false, 1024, 9, true>,  (const void*)k_ntt8<false, 1024, 10, true>};
+    for (const void* f : big) (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bigb);
+#endif
     attr_set = true;
   }
   // pass sizes: prefer multiples of 3 (whole radix-8 rounds), largest pass last
@@ -515,6 +543,7 @@ void launch_ntt(Prof& prof, hipStream_t s, const NttBatch& b, uint32_t logn, boo
   uint32_t s0 = 0;
   for (uint32_t p = 0; p < npass; p++) {
     uint32_t K = Ks[p];
+    const uint32_t lognt = K >= 9 ? 10 : 8, loge = lognt + 3;
     Ntt8Args a;
     bool first = p == 0;
     a.src = first ? b.src : b.dst;
@@ -529,7 +558,7 @@ void launch_ntt(Prof& prof, hipStream_t s, const NttBatch& b, uint32_t logn, boo
     a.s0 = s0;
     a.K = K;
     a.lo = dit ? s0 : logn - s0 - K;
-    a.logT = LOGE - K;
+    a.logT = loge - K;
     a.logTl = a.logT < a.lo ? a.logT : a.lo;
     a.tw_shift = logN - logn;
     // rounds of <= 3 bits, larger first
@@ -543,7 +572,11 @@ void launch_ntt(Prof& prof, hipStream_t s, const NttBatch& b, uint32_t logn, boo
       rem -= rb;
     }
     uint64_t groups = 1ull << (logn - K);
+#ifdef ZKP_NTT_POSFAST
+    dim3 grid((uint32_t)(groups >> a.logT), b.batches);
+#else
     dim3 grid(b.batches, (uint32_t)(groups >> a.logT));  // batch fastest (see k_ntt8)
+#endif
     size_t shmem = (size_t)(1u << K) * (1u << a.logT) * sizeof(felt);
     // compulsory bytes of this launch: every distinct input array once (the
     // coefficient arrays are shared by src_div coset batches, the scale table
@@ -554,23 +587,28 @@ void launch_ntt(Prof& prof, hipStream_t s, const NttBatch& b, uint32_t logn, boo
     const double bytes = arr * ((double)src_arrays + scale_rows + b.batches);
     // the pass over stages 0..2 (lo = 0): the trivial-twiddle variant
     const bool small = a.lo == 0;
-#define ZKP_NTT8(D, KK)                                                                                  \
-  LAUNCH(prof, D ? "ntt_dit" : "ntt_dif", s, bytes,                                                     \
-         if (small) hipLaunchKernelGGL((k_ntt8<D, 256, KK, true>), grid, dim3(256), shmem, s, a);         \
-         else hipLaunchKernelGGL((k_ntt8<D, 256, KK, false>), grid, dim3(256), shmem, s, a))
+#define ZKP_NTT8(D, NTT, KK)                                                                                   \
+  LAUNCH(prof, D ? "ntt_dit" : "ntt_dif", s, bytes,                                                           \
+         if (small) hipLaunchKernelGGL((k_ntt8<D, NTT, KK, true>), grid, dim3(NTT), shmem, s, a);              \
+         else hipLaunchKernelGGL((k_ntt8<D, NTT, KK, false>), grid, dim3(NTT), shmem, s, a))
     switch (K * 2 + (dit ? 1 : 0)) {
-      case 11: ZKP_NTT8(true, 5); break;
-      case 13: ZKP_NTT8(true, 6); break;
-      case 15: ZKP_NTT8(true, 7); break;
-      case 17: ZKP_NTT8(true, 8); break;
-      case 10: ZKP_NTT8(false, 5); break;
-      case 12: ZKP_NTT8(false, 6); break;
-      case 14: ZKP_NTT8(false, 7); break;
-      case 16: ZKP_NTT8(false, 8); break;
-      default: abort();  // launch_ntt only plans passes of 5..8 stages
+      case 11: ZKP_NTT8(true, 256, 5); break;
+      case 13: ZKP_NTT8(true, 256, 6); break;
+      case 15: ZKP_NTT8(true, 256, 7); break;
+      case 17: ZKP_NTT8(true, 256, 8); break;
+      case 10: ZKP_NTT8(false, 256, 5); break;
+      case 12: ZKP_NTT8(false, 256, 6); break;
+      case 14: ZKP_NTT8(false, 256, 7); break;
+      case 16: ZKP_NTT8(false, 256, 8); break;
+#if ZKP_NTT_KMAX > 8
+      case 19: ZKP_NTT8(true, 1024, 9); break;
+      case 21: ZKP_NTT8(true, 1024, 10); break;
+      case 18: ZKP_NTT8(false, 1024, 9); break;
+      case 20: ZKP_NTT8(false, 1024, 10); break;
+#endif
+      default: abort();  // launch_ntt only plans passes of 5..KMAX stages
     }
 #undef ZKP_NTT8
     s0 += K;
   }
 }
-
