@@ -271,6 +271,7 @@ struct zkp_ctx {
       it = it->first.compare(0, prefix.size(), prefix) == 0 ? cached.erase(it) : std::next(it);
   }
   uint64_t next_session = 0;
+  std::vector<hipEvent_t> up_ev;  // column-group upload events (pipelined host traces)
 
   zkp_comm* self = nullptr;
   zkp_comm* self_comm() {
@@ -286,6 +287,7 @@ struct zkp_ctx {
     if (pinned_p) (void)hipHostFree(pinned_p);
     if (ring_p) (void)hipHostFree(ring_p);
     for (auto e : prof.pool) (void)hipEventDestroy(e);
+    for (auto e : up_ev) (void)hipEventDestroy(e);
     if (ev_fork) (void)hipEventDestroy(ev_fork);
     if (ev_join) (void)hipEventDestroy(ev_join);
     if (side) (void)hipStreamDestroy(side);
@@ -842,9 +844,12 @@ const felt* fold_constants(zkp_ctx* ctx) {
   return deps;
 }
 
+// h_trace (nullable): the trace is still in host memory and d_trace is its
+// device buffer; the upload is pipelined with the trace interpolation and LDE
+// by column groups (wide traces), so PCIe overlaps the first stage's kernels.
 int prove_impl(zkp_ctx* ctx, zkp_comm* cm, int air_id, const felt* d_trace, uint32_t w, uint64_t n,
                const zkp_felt* pub_elems, uint64_t n_pub, const zkp_proof_options* o, uint8_t** proof,
-               uint64_t* proof_len, zkp_transcript* tr_out) {
+               uint64_t* proof_len, zkp_transcript* tr_out, const zkp_felt* h_trace = nullptr) {
   int rc = check_options(o);
   if (rc) return rc;
   if (n < 8 || (n & (n - 1)) || w == 0 || w > 255) return ZKP_ERR_TRACE_SHAPE;
@@ -924,10 +929,35 @@ int prove_impl(zkp_ctx* ctx, zkp_comm* cm, int air_id, const felt* d_trace, uint
   TreeShard ttree;
   bool coeffs_drawn = false;
   {
-    NttBatch ib{d_trace, coef, nullptr, n, n, 1, 1, w};
-    launch_ntt(pf, st, ib, logn, false, ctx->itws(logN), logN);
-    NttBatch lb{coef, tlde, Sj0, n, n, Bl, Bl, w * Bl};
-    launch_ntt(pf, st, lb, logn, true, ctx->tws(logN), logN);
+    // column groups: one for device-resident traces; host traces upload group g+1
+    // on the copy stream while the main stream interpolates and extends group g
+    const uint32_t groups = h_trace ? (w >= 16 ? 8u : (w >= 4 ? 4u : 1u)) : 1u;
+    const uint32_t cg = (w + groups - 1) / groups;
+    if (groups > 1 && ctx->up_ev.size() < groups) {
+      for (hipEvent_t e : ctx->up_ev) HIP_CHECK(hipEventDestroy(e));
+      ctx->up_ev.assign(groups, nullptr);
+      for (auto& e : ctx->up_ev) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    }
+    if (h_trace && groups > 1) {  // the copy stream starts after everything already queued
+      HIP_CHECK(hipEventRecord(ctx->ev_fork, st));
+      HIP_CHECK(hipStreamWaitEvent(ctx->side, ctx->ev_fork, 0));
+    }
+    for (uint32_t c0 = 0, g = 0; c0 < w; c0 += cg, g++) {
+      const uint32_t cw = c0 + cg <= w ? cg : w - c0;
+      felt* dcol = const_cast<felt*>(d_trace) + (size_t)c0 * n;
+      if (h_trace && groups > 1) {
+        HIP_CHECK(hipMemcpyAsync(dcol, h_trace + (size_t)c0 * n, (size_t)cw * n * 16, hipMemcpyHostToDevice,
+                                 ctx->side));
+        HIP_CHECK(hipEventRecord(ctx->up_ev[g], ctx->side));
+        HIP_CHECK(hipStreamWaitEvent(st, ctx->up_ev[g], 0));
+      } else if (h_trace) {
+        ctx->upload(dcol, h_trace, (size_t)w * n * 16);
+      }
+      NttBatch ib{dcol, coef + (size_t)c0 * n, nullptr, n, n, 1, 1, cw};
+      launch_ntt(pf, st, ib, logn, false, ctx->itws(logN), logN);
+      NttBatch lb{coef + (size_t)c0 * n, tlde + (size_t)c0 * Bl * n, Sj0, n, n, Bl, Bl, cw * Bl};
+      launch_ntt(pf, st, lb, logn, true, ctx->tws(logN), logN);
+    }
     // unsharded: the tree's last block also reseeds with the root and draws the
     // composition coefficients (MERKLE_TAIL_DRAW_COEFFS)
     MerkleTail draw{};
@@ -1429,8 +1459,8 @@ int zkp_prove(zkp_ctx* ctx, zkp_air_id air, const zkp_felt* trace, uint32_t widt
     if (!trace) return (int)ZKP_ERR_ARGUMENT;
     if (n < 8 || (n & (n - 1)) || width == 0 || width > 255) return (int)ZKP_ERR_TRACE_SHAPE;
     felt* d = ctx->buf<felt>("trace_in", (size_t)width * n);
-    ctx->upload(d, trace, (size_t)width * n * 16);
-    return prove_impl(ctx, ctx->self_comm(), air, d, width, n, pub, n_pub, opts, proof, proof_len, transcript);
+    return prove_impl(ctx, ctx->self_comm(), air, d, width, n, pub, n_pub, opts, proof, proof_len, transcript,
+                      trace);
   });
 }
 
@@ -1443,8 +1473,7 @@ int zkp_prove_sharded(zkp_ctx* ctx, zkp_comm* comm, zkp_air_id air, const zkp_fe
     if (!trace || !comm) return (int)ZKP_ERR_ARGUMENT;
     if (n < 8 || (n & (n - 1)) || width == 0 || width > 255) return (int)ZKP_ERR_TRACE_SHAPE;
     felt* d = ctx->buf<felt>("trace_in", (size_t)width * n);
-    ctx->upload(d, trace, (size_t)width * n * 16);
-    return prove_impl(ctx, comm, air, d, width, n, pub, n_pub, opts, proof, proof_len, transcript);
+    return prove_impl(ctx, comm, air, d, width, n, pub, n_pub, opts, proof, proof_len, transcript, trace);
   });
   // a rank that fails (argument checks included) releases peers blocked in a collective
   if (rc && comm) comm->abort();
