@@ -57,7 +57,7 @@ KERNEL_STAGES = {
     "ntt_dit": ("lde", "comp_lde"), "ntt_dif": ("intt", "comp_intt"), "deep": ("deep",),
     "eval_mimc": ("eval",), "eval_linear": ("eval",),
 }
-PMC_TAGS = ("r02", "r01")  # newest committed PMC summaries first
+PMC_TAGS = ("r02", "r01")  # newest committed PMC summaries first (scripts/profile_round.sh)
 
 
 def stage_bytes(w: int, n: int, B: int, ce: int, C: int, rem: int = 7, F: int = 16) -> dict:
