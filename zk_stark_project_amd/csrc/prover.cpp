@@ -271,7 +271,13 @@ struct zkp_ctx {
       it = it->first.compare(0, prefix.size(), prefix) == 0 ? cached.erase(it) : std::next(it);
   }
   uint64_t next_session = 0;
-  std::vector<hipEvent_t> up_ev;  // column-group upload events (pipelined host traces)
+  std::vector<hipEvent_t> up_ev;  // pipeline events (column-group uploads, per-column all-gathers)
+  void events(size_t k) {
+    if (up_ev.size() >= k) return;
+    for (hipEvent_t e : up_ev) HIP_CHECK(hipEventDestroy(e));
+    up_ev.assign(k, nullptr);
+    for (auto& e : up_ev) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  }
 
   zkp_comm* self = nullptr;
   zkp_comm* self_comm() {
@@ -933,11 +939,7 @@ int prove_impl(zkp_ctx* ctx, zkp_comm* cm, int air_id, const felt* d_trace, uint
     // on the copy stream while the main stream interpolates and extends group g
     const uint32_t groups = h_trace ? (w >= 16 ? 8u : (w >= 4 ? 4u : 1u)) : 1u;
     const uint32_t cg = (w + groups - 1) / groups;
-    if (groups > 1 && ctx->up_ev.size() < groups) {
-      for (hipEvent_t e : ctx->up_ev) HIP_CHECK(hipEventDestroy(e));
-      ctx->up_ev.assign(groups, nullptr);
-      for (auto& e : ctx->up_ev) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    }
+    if (groups > 1) ctx->events(groups);
     if (h_trace && groups > 1) {  // the copy stream starts after everything already queued
       HIP_CHECK(hipEventRecord(ctx->ev_fork, st));
       HIP_CHECK(hipStreamWaitEvent(ctx->side, ctx->ev_fork, 0));
@@ -1029,14 +1031,25 @@ int prove_impl(zkp_ctx* ctx, zkp_comm* cm, int air_id, const felt* d_trace, uint
     felt* slice = R > 1 ? ctx->buf<felt>("comp_ag_send", (size_t)C * nR) : acoef;
     launch_comp_dft(pf, st, recv, dblk, ctx->Si(logn, logB, logce), dcoefs, ce, C, logn, p0, nR, slice);
     if (R > 1) {
-      felt* ag = ctx->buf<felt>("comp_ag_recv", (size_t)C * n);
-      cm->all_gather(st, slice, ag, (size_t)C * nR * 16);
-      for (uint32_t m = 0; m < C; m++)  // [s][m][pl] -> column m, positions s*nR + pl
-        HIP_CHECK(hipMemcpy2DAsync(acoef + (size_t)m * n, nR * 16, ag + (size_t)m * nR, (size_t)C * nR * 16, nR * 16,
-                                   R, hipMemcpyDeviceToDevice, st));
+      // column by column: the all-gather of coefficient column m (rank s's slice of
+      // positions [s*nR, (s+1)*nR) lands at acoef + m*n + s*nR, i.e. the column in
+      // order) runs on the side stream while the main stream extends column m - 1
+      // (the largest exchange of a sharded proof, hidden behind the
+      // composition LDE)
+      ctx->events(C);
+      HIP_CHECK(hipEventRecord(ctx->ev_fork, st));
+      HIP_CHECK(hipStreamWaitEvent(ctx->side, ctx->ev_fork, 0));
+      for (uint32_t m = 0; m < C; m++) {
+        cm->all_gather(ctx->side, slice + (size_t)m * nR, acoef + (size_t)m * n, nR * 16);
+        HIP_CHECK(hipEventRecord(ctx->up_ev[m], ctx->side));
+        HIP_CHECK(hipStreamWaitEvent(st, ctx->up_ev[m], 0));
+        NttBatch lb{acoef + (size_t)m * n, clde + (size_t)m * Bl * n, Sj0, n, n, Bl, Bl, Bl};
+        launch_ntt(pf, st, lb, logn, true, ctx->tws(logN), logN);
+      }
+    } else {
+      NttBatch lb{acoef, clde, Sj0, n, n, Bl, Bl, C * Bl};
+      launch_ntt(pf, st, lb, logn, true, ctx->tws(logN), logN);
     }
-    NttBatch lb{acoef, clde, Sj0, n, n, Bl, Bl, C * Bl};
-    launch_ntt(pf, st, lb, logn, true, ctx->tws(logN), logN);
     MerkleTail draw{};  // unsharded: the tree's last block draws z (MERKLE_TAIL_DRAW_Z)
     draw.op = MERKLE_TAIL_DRAW_Z;
     draw.coin_seed = dt_seed;
