@@ -215,10 +215,11 @@ def make_workload(air: str, sharded: bool, log_n, blowup: int, seed_rank: int, c
                 ce=2, C=1, workload=f"GlobalUpdate AIR, {ndev} updates padded to 2^{log_n} rows, w=120 ({cfg})")
 
 
-def sharded_leg(ctx, rank: int, world: int, dist, local_rank: int, timeout_s: float = 120.0):
+def sharded_leg(ctx, rank: int, world: int, dist, local_rank: int, on_timeout=None, timeout_s: float = 120.0):
     """One C4 proof (MiMC 2^22, B = 8) split over all `world` ranks by LDE coset over
-    RCCL; timed like the headline (barrier + device sync, max over ranks). A watchdog
-    bounds it: a hung collective ends the process instead of the driver's run."""
+    RCCL; timed like the headline (barrier + device sync, max over ranks). Runs after
+    the headline line is built: a watchdog bounds it, and on a hung collective rank 0
+    prints the headline (with the sharded error) before every rank exits."""
     import torch
     from zk_stark_project_amd.replicas import timed_replicas
     from zk_stark_project_amd.sharded import rccl_group_comm
@@ -229,7 +230,10 @@ def sharded_leg(ctx, rank: int, world: int, dist, local_rank: int, timeout_s: fl
         if not done.wait(timeout_s):
             print(json.dumps({"error": f"sharded leg exceeded {timeout_s:.0f} s on rank {rank}"}), file=sys.stderr,
                   flush=True)
-            os._exit(3)
+            if on_timeout is not None:
+                on_timeout()
+            sys.stdout.flush()
+            os._exit(0)
     threading.Thread(target=watchdog, daemon=True).start()
     wl = make_workload("mimc", True, None, 8, 0, ctx)
     pub = wl["prover"].get_pub_inputs(wl["trace"]).to_elements()
@@ -337,16 +341,15 @@ def main():
         sus_n += 1
     sus_s = time.perf_counter() - t1
 
-    sharded_res = None
-    if world > 1 and not sharded and not args.no_sharded_leg:
-        try:
-            sharded_res = sharded_leg(ctx, rank, world, dist, local_rank)
-        except Exception as e:  # noqa: BLE001 — reported in the line, the headline stands
-            sharded_res = {"error": f"{type(e).__name__}: {e}"}
-
     if comm is not None:
         comm.close()
+    run_sharded = world > 1 and not sharded and not args.no_sharded_leg
     if rank != 0:
+        if run_sharded:  # collective with rank 0's leg below
+            try:
+                sharded_leg(ctx, rank, world, dist, local_rank)
+            except Exception:  # noqa: BLE001 — rank 0 reports it
+                pass
         if dist is not None:
             dist.destroy_process_group()
         return
@@ -444,8 +447,13 @@ def main():
         "verified_by_oracle": verified,
         "parity": "bit-exact vs the C oracle; parity vs winterfell 0.12 bytes unpinned (DESIGN.md §2)",
     }
-    if sharded_res is not None:
-        out["sharded"] = sharded_res
+    if run_sharded:
+        def headline_on_timeout():
+            print(json.dumps({**out, "sharded": {"error": "timed out (watchdog)"}}), flush=True)
+        try:
+            out["sharded"] = sharded_leg(ctx, rank, world, dist, local_rank, on_timeout=headline_on_timeout)
+        except Exception as e:  # noqa: BLE001 — reported in the line, the headline stands
+            out["sharded"] = {"error": f"{type(e).__name__}: {e}"}
     print(json.dumps(out), flush=True)
     if args.stats:
         for k, v in sorted(host_stages.items()):
