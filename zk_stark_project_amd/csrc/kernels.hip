@@ -1743,7 +1743,9 @@ void launch_grind(Prof& prof, hipStream_t s, const uint32_t* seed_words, const u
 void launch_grind_all(Prof& prof, hipStream_t s, const uint32_t* seed_dev, uint64_t base, uint64_t limit,
                       uint32_t bits, unsigned long long* result) {
   LAUNCH(prof, "grind", s, 0.0,
-         hipLaunchKernelGGL(k_grind_all, dim3(4096), dim3(TPB), 0, s, seed_dev, base, limit, bits, result));
+         // 1024 x 256 threads: 4 waves per SIMD, and 2^18 nonces per iteration keeps the
+         // overshoot past the minimum small (2^21 expected tries at the reference's 21 bits)
+         hipLaunchKernelGGL(k_grind_all, dim3(1024), dim3(TPB), 0, s, seed_dev, base, limit, bits, result));
 }
 
 void launch_query_positions(Prof& prof, hipStream_t s, const uint32_t* seed_dev, const unsigned long long* nonce,
