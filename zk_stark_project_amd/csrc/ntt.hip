@@ -104,10 +104,10 @@ struct Ntt8Args {
 
 // stage-major twiddles: level t holds w_{2^(t+1)}^j at tw[(2^t - 1) + j]
 template <bool DIT>
-__device__ __forceinline__ felt ntt_tw(const Ntt8Args& a, uint64_t j, uint32_t pbit) {
+__device__ __forceinline__ felt ntt_tw(const Ntt8Args& a, uint32_t j, uint32_t pbit) {
   uint32_t s = DIT ? a.s0 + pbit : a.s0 + a.K - 1 - pbit;
   uint32_t lev = DIT ? s : a.logn - 1 - s;
-  return a.tw[((1ull << lev) - 1) + j];
+  return a.tw[((1u << lev) - 1) + j];
 }
 
 template <bool DIT>
@@ -206,38 +206,44 @@ __global__ __launch_bounds__(NT) void k_ntt8(Ntt8Args a) {
 #endif
   const felt* src = a.src + (uint64_t)(bidx / a.src_div) * a.src_stride;
   felt* dst = a.dst + (uint64_t)bidx * a.dst_stride;
+#ifdef ZKP_EXP_NOSCALE  // timing experiment only: no coset-scale reads (wrong values)
+  const felt* scale = nullptr;
+#else
   const felt* scale = a.scale ? a.scale + ((uint64_t)(bidx % a.scale_mod) << a.logn) : nullptr;
+#endif
 #ifdef ZKP_NTT_POSFAST
   const uint64_t g0 = (uint64_t)blockIdx.x << logT;
 #else
   const uint64_t g0 = (uint64_t)blockIdx.y << logT;
 #endif
-  const uint64_t hi0 = g0 >> lo;
-  const uint64_t l0 = (Tl == T) ? (g0 & ((1ull << lo) - 1)) : 0;
+  const uint32_t hi0 = (uint32_t)(g0 >> lo);
+  const uint32_t l0 = (Tl == T) ? (uint32_t)(g0 & ((1ull << lo) - 1)) : 0;
   const uint32_t qmask = (1u << K) - 1;
   const uint32_t tid = threadIdx.x;
 
   // global address of block-local element (gg, q)
-  auto gaddr = [&](uint32_t gg, uint32_t q) -> uint64_t {
+  // element offsets within one array fit 32 bits (launch_ntt checks logn), so
+  // loads and stores take a scalar base + one 32-bit VGPR offset
+  auto gaddr = [&](uint32_t gg, uint32_t q) -> uint32_t {
     uint32_t hl = gg >> a.logTl, ll = gg & (Tl - 1);
-    return ((hi0 + hl) << (lo + K)) + ((uint64_t)q << lo) + l0 + ll;
+    return ((hi0 + hl) << (lo + K)) + (q << lo) + l0 + ll;
   };
   (void)qmask;
   // Passes whose groups have < 8 contiguous felts (lo < 3, e.g. the first DIT
   // pass) would make every lane of a direct load/store touch its own 128-B
   // line; those go through LDS in (ll, q, hl) order, contiguous along the wave.
   const bool staged = a.logTl < 3;
-  auto staged_elem = [&](uint32_t e, uint32_t& slot) -> uint64_t {
+  auto staged_elem = [&](uint32_t e, uint32_t& slot) -> uint32_t {
     uint32_t ll = e & (Tl - 1), rest = e >> a.logTl;
     uint32_t q = rest & ((1u << K) - 1), hl = rest >> K;
     slot = lidx(q, hl * Tl + ll);
-    return ((hi0 + hl) << (lo + K)) + ((uint64_t)q << lo) + l0 + ll;
+    return ((hi0 + hl) << (lo + K)) + (q << lo) + l0 + ll;
   };
   if (staged) {
 #pragma unroll
     for (int i = 0; i < 8; i++) {
       uint32_t slot;
-      uint64_t ad = staged_elem(tid + i * NT, slot);
+      uint32_t ad = staged_elem(tid + i * NT, slot);
 #ifdef ZKP_EXP_NOGMEM
       felt v = fp::make(ad, (uint64_t)i);
       if (scale) v = mul(v, v);
@@ -271,7 +277,7 @@ __global__ __launch_bounds__(NT) void k_ntt8(Ntt8Args a) {
       uint32_t extra = m >> rb, bf = m & ((1u << rb) - 1);
       uint32_t c = (extra << LOGNT) | tid;
       if (first && !staged) {  // straight from HBM (coalesced along gg), coset scale fused
-        uint64_t ad = gaddr(coord_gg(m), coord_q(m));
+        uint32_t ad = gaddr(coord_gg(m), coord_q(m));
 #ifdef ZKP_EXP_NOGMEM  // timing experiment only (scripts/ntt_experiments.sh): no HBM reads
         felt v = fp::make(ad, (uint64_t)m);
         if (scale) v = mul(v, v);
@@ -290,9 +296,9 @@ __global__ __launch_bounds__(NT) void k_ntt8(Ntt8Args a) {
 #else
     if constexpr (rb == 3) {
 #endif
-      const uint64_t l = l0 + (ggs[0] & (Tl - 1));
-      const uint64_t jb = ((uint64_t)qlow[0] << lo) | l;
-      const uint64_t jstep = 1ull << (b0 + lo);
+      const uint32_t l = l0 + (ggs[0] & (Tl - 1));
+      const uint32_t jb = (qlow[0] << lo) | l;
+      const uint32_t jstep = 1u << (b0 + lo);
       // stages 0..2 (b0 = 0, lo = 0, so jb = 0): 7 of the 12 products are by 1
       constexpr bool smallest = SMALL && (DIT ? first : last);
       if constexpr (DIT && smallest) {
@@ -324,14 +330,14 @@ __global__ __launch_bounds__(NT) void k_ntt8(Ntt8Args a) {
           bfly2<true>(x[0], x[2], w1a, x[1], x[3], w1b); bfly2<true>(x[4], x[6], w1a, x[5], x[7], w1b);
         }
         static_for<0, 2>([&](auto k2) {
-          felt w2a = ntt_tw<true>(a, jb | ((uint64_t)(2 * k2) << (b0 + lo)), b0 + 2);
-          felt w2b = ntt_tw<true>(a, jb | ((uint64_t)(2 * k2 + 1) << (b0 + lo)), b0 + 2);
+          felt w2a = ntt_tw<true>(a, jb | ((uint32_t)(2 * k2) << (b0 + lo)), b0 + 2);
+          felt w2b = ntt_tw<true>(a, jb | ((uint32_t)(2 * k2 + 1) << (b0 + lo)), b0 + 2);
           bfly2<true>(x[2 * k2], x[2 * k2 + 4], w2a, x[2 * k2 + 1], x[2 * k2 + 5], w2b);
         });
       } else {
         static_for<0, 2>([&](auto k2) {
-          felt w2a = ntt_tw<false>(a, jb | ((uint64_t)(2 * k2) << (b0 + lo)), b0 + 2);
-          felt w2b = ntt_tw<false>(a, jb | ((uint64_t)(2 * k2 + 1) << (b0 + lo)), b0 + 2);
+          felt w2a = ntt_tw<false>(a, jb | ((uint32_t)(2 * k2) << (b0 + lo)), b0 + 2);
+          felt w2b = ntt_tw<false>(a, jb | ((uint32_t)(2 * k2 + 1) << (b0 + lo)), b0 + 2);
           bfly2<false>(x[2 * k2], x[2 * k2 + 4], w2a, x[2 * k2 + 1], x[2 * k2 + 5], w2b);
         });
         {
@@ -357,10 +363,10 @@ __global__ __launch_bounds__(NT) void k_ntt8(Ntt8Args a) {
       } else {
 #pragma unroll
       for (int u = 0; u < 2; u++) {
-        const uint64_t l = l0 + (ggs[u] & (Tl - 1));
-        const uint64_t jb = ((uint64_t)qlow[u] << lo) | l;
+        const uint32_t l = l0 + (ggs[u] & (Tl - 1));
+        const uint32_t jb = (qlow[u] << lo) | l;
         felt w0 = ntt_tw<DIT>(a, jb, b0);
-        felt w1a = ntt_tw<DIT>(a, jb, b0 + 1), w1b = ntt_tw<DIT>(a, jb | (1ull << (b0 + lo)), b0 + 1);
+        felt w1a = ntt_tw<DIT>(a, jb, b0 + 1), w1b = ntt_tw<DIT>(a, jb | (1u << (b0 + lo)), b0 + 1);
         felt* y = x + 4 * u;
         if (DIT) {
           bfly2<true>(y[0], y[1], w0, y[2], y[3], w0);
@@ -377,7 +383,7 @@ __global__ __launch_bounds__(NT) void k_ntt8(Ntt8Args a) {
         uint32_t c = ((uint32_t)u << LOGNT) | tid;
         uint32_t gg = c & (T - 1);
         uint32_t ql = (c >> logT) & ((1u << b0) - 1);
-        const uint64_t jb = ((uint64_t)ql << lo) | (l0 + (gg & (Tl - 1)));
+        const uint32_t jb = (ql << lo) | (l0 + (gg & (Tl - 1)));
         bfly<DIT>(x[2 * u], x[2 * u + 1], ntt_tw<DIT>(a, jb, b0));
       }
     }
@@ -398,7 +404,7 @@ __global__ __launch_bounds__(NT) void k_ntt8(Ntt8Args a) {
 #pragma unroll
     for (int i = 0; i < 8; i++) {
       uint32_t slot;
-      uint64_t ad = staged_elem(tid + i * NT, slot);
+      uint32_t ad = staged_elem(tid + i * NT, slot);
 #ifdef ZKP_EXP_NOGMEM
       if (lds[slot].lo == 0x0123456789abcdefull) dst[ad] = lds[slot];
 #else
@@ -497,6 +503,7 @@ void launch_ntt(Prof& prof, hipStream_t s, const NttBatch& b, uint32_t logn, boo
   // (ZKP_NTT_KMAX=10 builds the 2-pass 2^20 schedule: measured slower, one
   // 128-KB block per CU cannot overlap its loads with compute)
   const uint32_t KMAX = logn >= 18 ? ZKP_NTT_KMAX : 8;
+  if (logN > 28) abort();  // k_ntt8 indexes arrays and twiddles with 32-bit element offsets
   if (logn < LOGE) {
     launch_ntt_radix2(prof, s, b, logn, dit, tw, logN);
     return;
@@ -515,6 +522,7 @@ void launch_ntt(Prof& prof, hipStream_t s, const NttBatch& b, uint32_t logn, boo
         (const void*)k_ntt8<false, 256, 5, true>,  (const void*)k_ntt8<false, 256, 6, true>,
         (const void*)k_ntt8<false, 256, 7, true>,  (const void*)k_ntt8<false, 256, 8, true>};
     for (const void* f : fns) (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)maxb);
+    (void)bigb;
 #if ZKP_NTT_KMAX > 8
     const void* big[] = {
         (const void*)k_ntt8<true, 1024, 9, false>,  (const void*)k_ntt8<true, 1024, 10, false>,
