@@ -498,11 +498,13 @@ void launch_ntt(Prof& prof, hipStream_t s, const NttBatch& b, uint32_t logn, boo
 #ifndef ZKP_NTT_KMAX
 #define ZKP_NTT_KMAX 8
 #endif
-  // passes of up to KMAX stages; passes of 9-10 stages run 1024-thread blocks of
-  // 8192 elements (128 KB LDS), so their strided groups still load 8-felt runs
-  // (ZKP_NTT_KMAX=10 builds the 2-pass 2^20 schedule: measured slower, one
-  // 128-KB block per CU cannot overlap its loads with compute)
-  const uint32_t KMAX = logn >= 18 ? ZKP_NTT_KMAX : 8;
+  // passes of up to KMAX stages. 2^17-2^18 run two passes of <= 9 stages instead
+  // of three: 9-stage passes use 512-thread blocks of 4096 elements (64 KB LDS,
+  // 2 blocks per CU = the same 4 waves/SIMD as 256-thread blocks; strided groups
+  // still load 8-felt runs), a third less HBM traffic for the same rounds.
+  // 10-stage passes need 1024-thread blocks (128 KB, one per CU: ZKP_NTT_KMAX=10
+  // builds the 2-pass 2^20 schedule, measured slower).
+  const uint32_t KMAX = (logn == 17 || logn == 18) ? 9 : (logn > 18 ? ZKP_NTT_KMAX : 8);
   if (logN > 28) abort();  // k_ntt8 indexes arrays and twiddles with 32-bit element offsets
   if (logn < LOGE) {
     launch_ntt_radix2(prof, s, b, logn, dit, tw, logN);
@@ -522,13 +524,13 @@ void launch_ntt(Prof& prof, hipStream_t s, const NttBatch& b, uint32_t logn, boo
         (const void*)k_ntt8<false, 256, 5, true>,  (const void*)k_ntt8<false, 256, 6, true>,
         (const void*)k_ntt8<false, 256, 7, true>,  (const void*)k_ntt8<false, 256, 8, true>};
     for (const void* f : fns) (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)maxb);
+    const void* k9[] = {(const void*)k_ntt8<true, 512, 9, false>, (const void*)k_ntt8<false, 512, 9, false>,
+                        (const void*)k_ntt8<true, 512, 9, true>, (const void*)k_ntt8<false, 512, 9, true>};
+    for (const void* f : k9) (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 4096 * 16);
     (void)bigb;
 #if ZKP_NTT_KMAX > 8
-    const void* big[] = {
-        (const void*)k_ntt8<true, 1024, 9, false>,  (const void*)k_ntt8<true, 1024, 10, false>,
-        (const void*)k_ntt8<false, 1024, 9, false>, (const void*)k_ntt8<false, 1024, 10, false>,
-        (const void*)k_ntt8<true, 1024, 9, true>,   (const void*)k_ntt8<true, 1024, 10, true>,
-        (const void*)k_ntt8<false, 1024, 9, true>,  (const void*)k_ntt8<false, 1024, 10, true>};
+    const void* big[] = {(const void*)k_ntt8<true, 1024, 10, false>, (const void*)k_ntt8<false, 1024, 10, false>,
+                         (const void*)k_ntt8<true, 1024, 10, true>, (const void*)k_ntt8<false, 1024, 10, true>};
     for (const void* f : big) (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bigb);
 #endif
     attr_set = true;
@@ -551,7 +553,7 @@ void launch_ntt(Prof& prof, hipStream_t s, const NttBatch& b, uint32_t logn, boo
   uint32_t s0 = 0;
   for (uint32_t p = 0; p < npass; p++) {
     uint32_t K = Ks[p];
-    const uint32_t lognt = K >= 9 ? 10 : 8, loge = lognt + 3;
+    const uint32_t lognt = K >= 10 ? 10 : (K == 9 ? 9 : 8), loge = lognt + 3;
     Ntt8Args a;
     bool first = p == 0;
     a.src = first ? b.src : b.dst;
@@ -608,10 +610,10 @@ void launch_ntt(Prof& prof, hipStream_t s, const NttBatch& b, uint32_t logn, boo
       case 12: ZKP_NTT8(false, 256, 6); break;
       case 14: ZKP_NTT8(false, 256, 7); break;
       case 16: ZKP_NTT8(false, 256, 8); break;
+      case 19: ZKP_NTT8(true, 512, 9); break;
+      case 18: ZKP_NTT8(false, 512, 9); break;
 #if ZKP_NTT_KMAX > 8
-      case 19: ZKP_NTT8(true, 1024, 9); break;
       case 21: ZKP_NTT8(true, 1024, 10); break;
-      case 18: ZKP_NTT8(false, 1024, 9); break;
       case 20: ZKP_NTT8(false, 1024, 10); break;
 #endif
       default: abort();  // launch_ntt only plans passes of 5..KMAX stages
