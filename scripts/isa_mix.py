@@ -35,8 +35,8 @@ def demangle(names):
     return dict(zip(names, out))
 
 
-def main(obj):
-    txt = disasm(obj)
+def main(objs):
+    txt = "\n".join(disasm(o) for o in objs)
     cur, per = None, collections.defaultdict(collections.Counter)
     for line in txt.splitlines():
         m = re.match(r"^[0-9a-f]+ <(.+)>:", line)
@@ -59,5 +59,5 @@ def main(obj):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1] if len(sys.argv) > 1 else os.path.join(os.path.dirname(__file__), "..", "zk_stark_project_amd",
-                                                             "csrc", "build", "kernels.o"))
+    build = os.path.join(os.path.dirname(__file__), "..", "zk_stark_project_amd", "csrc", "build")
+    main(sys.argv[1:] or [os.path.join(build, "kernels.o"), os.path.join(build, "ntt.o")])
