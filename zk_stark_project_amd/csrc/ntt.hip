@@ -187,13 +187,29 @@ __global__ __launch_bounds__(NT) void k_ntt8(Ntt8Args a) {
   constexpr uint32_t LOGNT = NT == 1024 ? 10 : (NT == 512 ? 9 : 8);
   constexpr uint32_t logT = LOGNT + 3 - KC;  // E = NT * 8 elements per block
   constexpr uint32_t T = 1u << logT;
-  static_assert(T >= 8, "the LDS swizzle needs rows of >= 8 felts");
+  static_assert(T >= 4, "the LDS swizzle needs rows of >= 4 felts");
   const uint32_t Tl = 1u << a.logTl, lo = a.lo;
   // LDS rows of T felts (T >= 8), XOR-swizzled by the row's low 3 bits: a wave's
   // 8-lane groups then hit 8 distinct 16-B bank slots both when lanes walk a row
   // (compute rounds) and when they walk down a column (staged loads, Tl = 1),
   // with no padding: 2048 felts = 32 KB per block, 5 blocks per CU
-  auto lidx = [](uint32_t q, uint32_t x) -> uint32_t { return q * T + (x ^ (q & 7u)); };
+  // Rows of 4 felts (10-stage passes in 512-thread blocks) cover 4 of the 16-B
+  // slots of a bank line. The row's low two bits are XORed with (b2^b3, b2^b5)
+  // and the felt index with (b1, b2^b3): every 8-lane ds_write_b128 group and
+  // every 16-lane ds_read_b128 group (MI355X_MICROARCH.md §LDS) then hits
+  // distinct slots, in all compute rounds of both directions (whose two or four
+  // rows per group differ in the row bits 0-5 that those rounds spread) and in
+  // the staged column walks (checked exhaustively by tests/native/lds_swizzle.py).
+  // (Fully conflict-free layouts for the 8-felt and >= 32-felt rows exist —
+  // tests/native/lds_swizzle.py — but measured no faster: DESIGN.md §4.)
+  auto lidx = [](uint32_t q, uint32_t x) -> uint32_t {
+    if constexpr (T >= 8) {
+      return q * T + (x ^ (q & 7u));
+    } else {
+      const uint32_t b1 = (q >> 1) & 1u, b23 = ((q >> 2) ^ (q >> 3)) & 1u, b25 = ((q >> 2) ^ (q >> 5)) & 1u;
+      return (q ^ (b23 | (b25 << 1))) * T + (x ^ (b1 | (b23 << 1)));
+    }
+  };
   // grid: x = batch (fastest in dispatch order), y = position block. The
   // batches of one position block run back to back, dealt round-robin over the
   // 8 XCDs: with B = 8 cosets batch b = col*B + j lands on XCD j, so the
@@ -232,7 +248,7 @@ __global__ __launch_bounds__(NT) void k_ntt8(Ntt8Args a) {
   // Passes whose groups have < 8 contiguous felts (lo < 3, e.g. the first DIT
   // pass) would make every lane of a direct load/store touch its own 128-B
   // line; those go through LDS in (ll, q, hl) order, contiguous along the wave.
-  const bool staged = a.logTl < 3;
+  const bool staged = a.logTl < (T >= 8 ? 3u : 2u);  // rows of 4: 64-B runs go direct
   auto staged_elem = [&](uint32_t e, uint32_t& slot) -> uint32_t {
     uint32_t ll = e & (Tl - 1), rest = e >> a.logTl;
     uint32_t q = rest & ((1u << K) - 1), hl = rest >> K;
@@ -502,9 +518,9 @@ void launch_ntt(Prof& prof, hipStream_t s, const NttBatch& b, uint32_t logn, boo
   // of three: 9-stage passes use 512-thread blocks of 4096 elements (64 KB LDS,
   // 2 blocks per CU = the same 4 waves/SIMD as 256-thread blocks; strided groups
   // still load 8-felt runs), a third less HBM traffic for the same rounds.
-  // 10-stage passes need 1024-thread blocks (128 KB, one per CU: ZKP_NTT_KMAX=10
-  // builds the 2-pass 2^20 schedule, measured slower).
-  const uint32_t KMAX = (logn == 17 || logn == 18) ? 9 : (logn > 18 ? ZKP_NTT_KMAX : 8);
+  // 10-stage passes (2^19-2^20 in two passes, ZKP_NTT_KMAX=10) use the same
+  // 512-thread blocks with rows of 4 felts (see k_ntt8's lidx).
+  const uint32_t KMAX = (logn == 17 || logn == 18) ? 9 : (logn == 19 || logn == 20) ? ZKP_NTT_KMAX : 8;
   if (logN > 28) abort();  // k_ntt8 indexes arrays and twiddles with 32-bit element offsets
   if (logn < LOGE) {
     launch_ntt_radix2(prof, s, b, logn, dit, tw, logN);
@@ -513,7 +529,7 @@ void launch_ntt(Prof& prof, hipStream_t s, const NttBatch& b, uint32_t logn, boo
   uint32_t npass = (logn + KMAX - 1) / KMAX;
   static bool attr_set = false;
   if (!attr_set) {
-    size_t maxb = (size_t)(1u << LOGE) * sizeof(felt), bigb = (size_t)(1u << 13) * sizeof(felt);
+    size_t maxb = (size_t)(1u << LOGE) * sizeof(felt);
     const void* fns[] = {
         (const void*)k_ntt8<true, 256, 5, false>,  (const void*)k_ntt8<true, 256, 6, false>,
         (const void*)k_ntt8<true, 256, 7, false>,  (const void*)k_ntt8<true, 256, 8, false>,
@@ -524,15 +540,11 @@ void launch_ntt(Prof& prof, hipStream_t s, const NttBatch& b, uint32_t logn, boo
         (const void*)k_ntt8<false, 256, 5, true>,  (const void*)k_ntt8<false, 256, 6, true>,
         (const void*)k_ntt8<false, 256, 7, true>,  (const void*)k_ntt8<false, 256, 8, true>};
     for (const void* f : fns) (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)maxb);
-    const void* k9[] = {(const void*)k_ntt8<true, 512, 9, false>, (const void*)k_ntt8<false, 512, 9, false>,
-                        (const void*)k_ntt8<true, 512, 9, true>, (const void*)k_ntt8<false, 512, 9, true>};
+    const void* k9[] = {(const void*)k_ntt8<true, 512, 9, false>,  (const void*)k_ntt8<false, 512, 9, false>,
+                        (const void*)k_ntt8<true, 512, 9, true>,   (const void*)k_ntt8<false, 512, 9, true>,
+                        (const void*)k_ntt8<true, 512, 10, false>, (const void*)k_ntt8<false, 512, 10, false>,
+                        (const void*)k_ntt8<true, 512, 10, true>,  (const void*)k_ntt8<false, 512, 10, true>};
     for (const void* f : k9) (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 4096 * 16);
-    (void)bigb;
-#if ZKP_NTT_KMAX > 8
-    const void* big[] = {(const void*)k_ntt8<true, 1024, 10, false>, (const void*)k_ntt8<false, 1024, 10, false>,
-                         (const void*)k_ntt8<true, 1024, 10, true>, (const void*)k_ntt8<false, 1024, 10, true>};
-    for (const void* f : big) (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bigb);
-#endif
     attr_set = true;
   }
   // pass sizes: prefer multiples of 3 (whole radix-8 rounds), largest pass last
@@ -553,7 +565,9 @@ void launch_ntt(Prof& prof, hipStream_t s, const NttBatch& b, uint32_t logn, boo
   uint32_t s0 = 0;
   for (uint32_t p = 0; p < npass; p++) {
     uint32_t K = Ks[p];
-    const uint32_t lognt = K >= 10 ? 10 : (K == 9 ? 9 : 8), loge = lognt + 3;
+    // 9 stages: 512 threads x 8 = 4096 elements, rows of 8; 10 stages: 512 x 8,
+    // rows of 4 (64 KB either way: 2 blocks per CU)
+    const uint32_t lognt = K >= 9 ? 9 : 8, loge = lognt + 3;
     Ntt8Args a;
     bool first = p == 0;
     a.src = first ? b.src : b.dst;
@@ -612,10 +626,8 @@ void launch_ntt(Prof& prof, hipStream_t s, const NttBatch& b, uint32_t logn, boo
       case 16: ZKP_NTT8(false, 256, 8); break;
       case 19: ZKP_NTT8(true, 512, 9); break;
       case 18: ZKP_NTT8(false, 512, 9); break;
-#if ZKP_NTT_KMAX > 8
-      case 21: ZKP_NTT8(true, 1024, 10); break;
-      case 20: ZKP_NTT8(false, 1024, 10); break;
-#endif
+      case 21: ZKP_NTT8(true, 512, 10); break;
+      case 20: ZKP_NTT8(false, 512, 10); break;
       default: abort();  // launch_ntt only plans passes of 5..KMAX stages
     }
 #undef ZKP_NTT8
