@@ -176,7 +176,10 @@ __device__ __forceinline__ uint32_t sel4(uint32_t q, uint32_t x0, uint32_t x1, u
   const uint32_t lo = (q & 1) ? x1 : x0, hi = (q & 1) ? x3 : x2;
   return (q & 2) ? hi : lo;
 }
-__device__ __forceinline__ void merge_quad(const uint32_t m[16], uint32_t q, uint32_t& o0, uint32_t& o1) {
+// One BLAKE3 compression (chunk counter 0, 64-byte block) by a quad: lane q
+// holds chaining-value words q (a) and 4+q (b) in and out.
+__device__ __forceinline__ void compress_quad(const uint32_t m[16], uint32_t q, uint32_t flags, uint32_t& a,
+                                              uint32_t& b) {
   constexpr uint8_t S[7][16] = {{0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15},
                                 {2, 6, 3, 10, 7, 0, 4, 13, 1, 11, 12, 5, 9, 14, 15, 8},
                                 {3, 4, 10, 12, 13, 2, 7, 14, 6, 5, 9, 0, 11, 15, 8, 1},
@@ -184,10 +187,8 @@ __device__ __forceinline__ void merge_quad(const uint32_t m[16], uint32_t q, uin
                                 {12, 13, 9, 11, 15, 10, 14, 8, 7, 2, 5, 3, 0, 1, 6, 4},
                                 {9, 14, 11, 5, 8, 12, 15, 1, 13, 3, 0, 10, 2, 6, 4, 7},
                                 {11, 15, 5, 0, 1, 9, 8, 6, 14, 10, 2, 12, 3, 4, 7, 13}};
-  uint32_t a = sel4(q, b3::iv(0), b3::iv(1), b3::iv(2), b3::iv(3));
-  uint32_t b = sel4(q, b3::iv(4), b3::iv(5), b3::iv(6), b3::iv(7));
-  uint32_t c = a;                                    // v[8..12) = IV[0..4)
-  uint32_t d = sel4(q, 0u, 0u, 64u, b3::CHUNK_START | b3::CHUNK_END | b3::ROOT);  // counter, block_len, flags
+  uint32_t c = sel4(q, b3::iv(0), b3::iv(1), b3::iv(2), b3::iv(3));  // v[8..12) = IV[0..4)
+  uint32_t d = sel4(q, 0u, 0u, 64u, flags);                          // counter, block_len, flags
 #define B3Q_G(x, y)                 \
   a = a + b + (x);                  \
   d = b3::rotr(d ^ a, 16);          \
@@ -211,8 +212,37 @@ __device__ __forceinline__ void merge_quad(const uint32_t m[16], uint32_t q, uin
     d = quad_rot<1>(d);
   }
 #undef B3Q_G
-  o0 = a ^ c;
-  o1 = b ^ d;
+  a ^= c;
+  b ^= d;
+}
+
+__device__ __forceinline__ void merge_quad(const uint32_t m[16], uint32_t q, uint32_t& o0, uint32_t& o1) {
+  o0 = sel4(q, b3::iv(0), b3::iv(1), b3::iv(2), b3::iv(3));
+  o1 = sel4(q, b3::iv(4), b3::iv(5), b3::iv(6), b3::iv(7));
+  compress_quad(m, q, b3::CHUNK_START | b3::CHUNK_END | b3::ROOT, o0, o1);
+}
+
+// Quad-cooperative digest of one FRI row of 16 felts (256 bytes: one chunk of
+// four blocks, hash_felts' nf <= 64 case); lane q returns words q and 4+q.
+__device__ __forceinline__ void fri_leaf_quad(const MerkleArgs& a, uint64_t i, uint32_t q, uint32_t& o0,
+                                              uint32_t& o1) {
+  const felt* base = a.src + ((i & ((1ull << a.logB) - 1)) * 16) * a.R + (i >> a.logB);
+  o0 = sel4(q, b3::iv(0), b3::iv(1), b3::iv(2), b3::iv(3));
+  o1 = sel4(q, b3::iv(4), b3::iv(5), b3::iv(6), b3::iv(7));
+#pragma unroll
+  for (uint32_t blk = 0; blk < 4; blk++) {
+    uint32_t m[16];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const felt v = base[(4 * blk + k) * a.R];
+      m[4 * k + 0] = (uint32_t)v.lo;
+      m[4 * k + 1] = (uint32_t)(v.lo >> 32);
+      m[4 * k + 2] = (uint32_t)v.hi;
+      m[4 * k + 3] = (uint32_t)(v.hi >> 32);
+    }
+    const uint32_t fl = (blk == 0 ? b3::CHUNK_START : 0u) | (blk == 3 ? (b3::CHUNK_END | b3::ROOT) : 0u);
+    compress_quad(m, q, fl, o0, o1);
+  }
 }
 
 __device__ __forceinline__ void merge8(const uint32_t l[8], const uint32_t r[8], uint32_t out[8]) {
@@ -225,29 +255,54 @@ __device__ __forceinline__ void merge8(const uint32_t l[8], const uint32_t r[8],
 
 __device__ void merkle_tail_op(const MerkleTail& tl, const uint32_t* root);
 
-template <int MODE>
+// QUAD (MODE 1 with 16-felt rows only): 64 leaves per block, each hashed by a
+// quad of lanes (compress_quad), so a small FRI layer's leaf stage is four
+// short-chain compressions instead of eight serial ones per lane; the layers
+// below 2^16 rows are latency-bound, not throughput-bound.
+template <int MODE, bool QUAD = false>
 __global__ __launch_bounds__(256) void k_merkle_fused(MerkleArgs a) {
   __shared__ uint32_t sd[256 * 9];
   const uint32_t t = threadIdx.x;
   const uint64_t L = a.L;
-  const uint64_t cnt = L < 512 ? L : 512;          // leaves in this block's subtree
-  const uint64_t base = (uint64_t)blockIdx.x * 512;
-  uint32_t m[8];
-  if (2 * t < cnt) {
-    uint32_t d0[8], d1[8];
-    merkle_leaf<MODE>(a, base + 2 * t, d0);
-    merkle_leaf<MODE>(a, base + 2 * t + 1, d1);
-    if (MODE != 2) {
-      store_digest(a.nodes + (L + base + 2 * t) * 8, d0);
-      store_digest(a.nodes + (L + base + 2 * t + 1) * 8, d1);
+  constexpr uint64_t LB = QUAD ? 64 : 512;        // leaves per block
+  const uint64_t cnt = L < LB ? L : LB;           // leaves in this block's subtree
+  const uint64_t base = (uint64_t)blockIdx.x * LB;
+  uint64_t lvl, lbase;
+  uint32_t s0;  // nodes of the level above the one held in sd[]
+  if constexpr (QUAD) {
+    const uint32_t nd = t >> 2, q = t & 3;
+    if (nd < cnt) {  // the 4 lanes of a quad are active together (DPP)
+      uint32_t o0, o1;
+      fri_leaf_quad(a, base + nd, q, o0, o1);
+      sd[nd * 9 + q] = o0;
+      sd[nd * 9 + 4 + q] = o1;
+      uint32_t* dst = a.nodes + (L + base + nd) * 8;
+      dst[q] = o0;
+      dst[4 + q] = o1;
     }
-    merge8(d0, d1, m);
-    store_digest(a.nodes + ((L >> 1) + (base >> 1) + t) * 8, m);
+    lvl = L;
+    lbase = base;
+    s0 = (uint32_t)(cnt >> 1);
+  } else {
+    uint32_t m[8];
+    if (2 * t < cnt) {
+      uint32_t d0[8], d1[8];
+      merkle_leaf<MODE>(a, base + 2 * t, d0);
+      merkle_leaf<MODE>(a, base + 2 * t + 1, d1);
+      if (MODE != 2) {
+        store_digest(a.nodes + (L + base + 2 * t) * 8, d0);
+        store_digest(a.nodes + (L + base + 2 * t + 1) * 8, d1);
+      }
+      merge8(d0, d1, m);
+      store_digest(a.nodes + ((L >> 1) + (base >> 1) + t) * 8, m);
 #pragma unroll
-    for (int i = 0; i < 8; i++) sd[t * 9 + i] = m[i];
+      for (int i = 0; i < 8; i++) sd[t * 9 + i] = m[i];
+    }
+    lvl = L >> 1;
+    lbase = base >> 1;
+    s0 = (uint32_t)(cnt >> 2);
   }
-  uint64_t lvl = L >> 1, lbase = base >> 1;
-  for (uint32_t s = (uint32_t)(cnt >> 2); s >= 1; s >>= 1) {
+  for (uint32_t s = s0; s >= 1; s >>= 1) {
     __syncthreads();
     if (s <= 64) {  // narrow level: one quad per node
       const uint32_t nd = t >> 2, q = t & 3;
@@ -1425,24 +1480,17 @@ __global__ __launch_bounds__(TPB) void k_fri_fold16(const felt* __restrict__ E, 
     v[blk + 1] = sub(x, y);
   }
   felt beta = mul(*alpha_p, mul(off_inv, itw_lev[r]));
-  // Horner over k = 15..0 with u_k = v[rev4(k)]
-  // u_k = v[rev4(k)], rev4 = {0,8,4,12,2,10,6,14,1,9,5,13,3,11,7,15}
-  felt acc = v[15];
-  acc = add(mul(acc, beta), v[7]);
-  acc = add(mul(acc, beta), v[11]);
-  acc = add(mul(acc, beta), v[3]);
-  acc = add(mul(acc, beta), v[13]);
-  acc = add(mul(acc, beta), v[5]);
-  acc = add(mul(acc, beta), v[9]);
-  acc = add(mul(acc, beta), v[1]);
-  acc = add(mul(acc, beta), v[14]);
-  acc = add(mul(acc, beta), v[6]);
-  acc = add(mul(acc, beta), v[10]);
-  acc = add(mul(acc, beta), v[2]);
-  acc = add(mul(acc, beta), v[12]);
-  acc = add(mul(acc, beta), v[4]);
-  acc = add(mul(acc, beta), v[8]);
-  acc = add(mul(acc, beta), v[0]);
+  // sum_k u_k beta^k with u_k = v[rev4(k)], by Estrin's scheme: 4 dependent
+  // products instead of Horner's 15 (the small layers are latency-bound; the
+  // field is exact, so any evaluation order gives the same canonical value)
+  constexpr int RV[16] = {0, 8, 4, 12, 2, 10, 6, 14, 1, 9, 5, 13, 3, 11, 7, 15};
+  const felt b2 = mul(beta, beta), b4 = mul(b2, b2), b8 = mul(b4, b4);
+  felt p[8];
+#pragma unroll
+  for (int j = 0; j < 8; j++) p[j] = add(v[RV[2 * j]], mul(v[RV[2 * j + 1]], beta));
+#pragma unroll
+  for (int j = 0; j < 4; j++) p[j] = add(p[2 * j], mul(p[2 * j + 1], b2));
+  const felt acc = add(add(p[0], mul(p[1], b4)), mul(add(p[2], mul(p[3], b4)), b8));
   out[q] = mul(acc, eps_inv[8]);
 }
 
@@ -1694,6 +1742,19 @@ bool launch_merkle_fri(Prof& prof, hipStream_t s, const felt* E, uint64_t m16, u
   a.cols = F;
   a.nodes = nodes;
   a.L = R;
+  static const bool no_quad = getenv("ZKP_NO_QUAD_LEAVES") != nullptr;  // A/B switch
+  if (F == 16 && R <= (1ull << 12) && !no_quad) {
+    // small layers (<= 2^12 rows): one quad of lanes per row, 64 rows and 6 levels
+    // per block. At 2^15 rows the quads' extra instructions made it slower
+    // (72 vs 53 us); at 2^11 / 2^7 / 2^3 rows it is faster (30/22/21 vs 40/34/29 us)
+    uint64_t blocks = (R + 63) / 64;
+    const bool finish = tail && tail->done && blocks <= 512;
+    if (finish) a.tail = *tail;
+    LAUNCH(prof, "merkle_fri", s, (double)R * (F * 16.0 + 64.0),
+           hipLaunchKernelGGL((k_merkle_fused<1, true>), dim3((uint32_t)blocks), dim3(256), 0, s, a));
+    if (finish) return true;
+    return merkle_upper(prof, s, nodes, blocks, tail);
+  }
   if (R <= (1ull << 16)) {
     // small layers: a lane subtree would serialise 19 compressions per lane on a
     // few waves; hash 2 rows per thread and build 9 levels per block instead
