@@ -1435,13 +1435,9 @@ __global__ __launch_bounds__(TPB) void k_deep(DeepArgs a, const felt* __restrict
 // Layer evaluations are coset-major (coset jl of Bl, m = 16*m16 positions):
 // local row q = jl*m16 + t' is the natural row r = (j0 + jl) + B*t' whose 16
 // values sit at positions t' + k*m16 of the same coset; out is coset-major.
-__global__ __launch_bounds__(TPB) void k_fri_fold16(const felt* __restrict__ E, uint64_t rows, uint32_t logm16,
-                                                    uint32_t j0, uint32_t logB, const felt* __restrict__ alpha_p,
-                                                    felt off_inv,
-                                                    const felt* __restrict__ itw_lev,
-                                                    const felt* __restrict__ eps_inv, felt* __restrict__ out) {
-  const uint64_t q = blockIdx.x * (uint64_t)TPB + threadIdx.x;
-  if (q >= rows) return;
+__device__ __forceinline__ felt fri_fold_row(const felt* __restrict__ E, uint64_t q, uint32_t logm16, uint32_t j0,
+                                             uint32_t logB, const felt* alpha_p, felt off_inv,
+                                             const felt* __restrict__ itw_lev, const felt* __restrict__ eps_inv) {
   const uint64_t m16 = 1ull << logm16;
   const uint64_t jl = q >> logm16, tp = q & (m16 - 1);
   const uint64_t r = (j0 + jl) + (tp << logB);
@@ -1480,18 +1476,120 @@ __global__ __launch_bounds__(TPB) void k_fri_fold16(const felt* __restrict__ E, 
     v[blk + 1] = sub(x, y);
   }
   felt beta = mul(*alpha_p, mul(off_inv, itw_lev[r]));
-  // sum_k u_k beta^k with u_k = v[rev4(k)], by Estrin's scheme: 4 dependent
-  // products instead of Horner's 15 (the small layers are latency-bound; the
-  // field is exact, so any evaluation order gives the same canonical value)
-  constexpr int RV[16] = {0, 8, 4, 12, 2, 10, 6, 14, 1, 9, 5, 13, 3, 11, 7, 15};
-  const felt b2 = mul(beta, beta), b4 = mul(b2, b2), b8 = mul(b4, b4);
-  felt p[8];
+  // Horner over k = 15..0 with u_k = v[rev4(k)], rev4 = {0,8,4,12,2,10,6,14,1,9,5,13,3,11,7,15}
+  // (Estrin's scheme measured slower: 18 products instead of 15, and one wave
+  // per SIMD issues in order, so the shorter chain buys nothing)
+  felt acc = v[15];
+  acc = add(mul(acc, beta), v[7]);
+  acc = add(mul(acc, beta), v[11]);
+  acc = add(mul(acc, beta), v[3]);
+  acc = add(mul(acc, beta), v[13]);
+  acc = add(mul(acc, beta), v[5]);
+  acc = add(mul(acc, beta), v[9]);
+  acc = add(mul(acc, beta), v[1]);
+  acc = add(mul(acc, beta), v[14]);
+  acc = add(mul(acc, beta), v[6]);
+  acc = add(mul(acc, beta), v[10]);
+  acc = add(mul(acc, beta), v[2]);
+  acc = add(mul(acc, beta), v[12]);
+  acc = add(mul(acc, beta), v[4]);
+  acc = add(mul(acc, beta), v[8]);
+  acc = add(mul(acc, beta), v[0]);
+  return mul(acc, eps_inv[8]);
+}
+
+__global__ __launch_bounds__(TPB) void k_fri_fold16(const felt* __restrict__ E, uint64_t rows, uint32_t logm16,
+                                                    uint32_t j0, uint32_t logB, const felt* __restrict__ alpha_p,
+                                                    felt off_inv,
+                                                    const felt* __restrict__ itw_lev,
+                                                    const felt* __restrict__ eps_inv, felt* __restrict__ out) {
+  const uint64_t q = blockIdx.x * (uint64_t)TPB + threadIdx.x;
+  if (q >= rows) return;
+  out[q] = fri_fold_row(E, q, logm16, j0, logB, alpha_p, off_inv, itw_lev, eps_inv);
+}
+
+// The FRI tail in one 512-thread block (world 1): for each layer of <= 128
+// rows, quad-hashed leaves -> tree (quad merges, levels in LDS, every node
+// written) -> coin step (alpha, root) -> fold into the next layer; then the
+// remainder (as k_fri_remainder). Replaces 2 launches per small layer + the
+// remainder launch, each of which costs its ~15-25 us launch/latency floor.
+__global__ __launch_bounds__(512) void k_fri_tail(FriTailArgs a) {
+  __shared__ uint32_t sd[128 * 9];
+  __shared__ felt s_c[256];
+  __shared__ uint32_t s_cv[32][8];
+  const uint32_t t = threadIdx.x, nd = t >> 2, q = t & 3;
+  for (uint32_t l = 0; l < a.nl; l++) {
+    const FriTailLayer y = a.ly[l];
+    const uint32_t R = 1u << (y.logm16 + a.logB);  // rows = leaves (<= 128, host-checked)
+    MerkleArgs ma{};
+    ma.src = y.E;
+    ma.R = 1ull << y.logm16;
+    ma.logB = a.logB;
+    ma.cols = 16;
+    if (nd < R) {  // whole quads
+      uint32_t o0, o1;
+      fri_leaf_quad(ma, nd, q, o0, o1);
+      sd[nd * 9 + q] = o0;
+      sd[nd * 9 + 4 + q] = o1;
+      uint32_t* dst = y.nodes + (uint64_t)(R + nd) * 8;
+      dst[q] = o0;
+      dst[4 + q] = o1;
+    }
+    for (uint32_t s = R >> 1; s >= 1; s >>= 1) {
+      __syncthreads();
+      uint32_t o0 = 0, o1 = 0;
+      if (nd < s) {
+        uint32_t mm[16];
 #pragma unroll
-  for (int j = 0; j < 8; j++) p[j] = add(v[RV[2 * j]], mul(v[RV[2 * j + 1]], beta));
+        for (int i = 0; i < 8; i++) { mm[i] = sd[(2 * nd) * 9 + i]; mm[8 + i] = sd[(2 * nd + 1) * 9 + i]; }
+        merge_quad(mm, q, o0, o1);
+      }
+      __syncthreads();
+      if (nd < s) {
+        sd[nd * 9 + q] = o0;
+        sd[nd * 9 + 4 + q] = o1;
+        uint32_t* dst = y.nodes + (uint64_t)(s + nd) * 8;
+        dst[q] = o0;
+        dst[4 + q] = o1;
+      }
+    }
+    __syncthreads();
+    if (t == 0) {
+      uint32_t r[8];
 #pragma unroll
-  for (int j = 0; j < 4; j++) p[j] = add(p[2 * j], mul(p[2 * j + 1], b2));
-  const felt acc = add(add(p[0], mul(p[1], b4)), mul(add(p[2], mul(p[3], b4)), b8));
-  out[q] = mul(acc, eps_inv[8]);
+      for (int i = 0; i < 8; i++) r[i] = sd[i];  // the root (node 1)
+      coin_fri_step(a.coin_seed, r, y.alpha_out, y.root_out);
+    }
+    __threadfence();  // alpha (and this layer's fold output below) visible block-wide
+    __syncthreads();
+    if (t < R) y.out[t] = fri_fold_row(y.E, t, y.logm16, 0, a.logB, y.alpha_out, y.off_inv, y.lev, a.eps_inv);
+    __threadfence();
+    __syncthreads();
+  }
+  // remainder: interpolate the last layer (D = m * B points) into ncoef = m
+  // coefficients, commit, reseed (k_fri_remainder)
+  const uint32_t m = a.rem_m, D = m << a.logB;
+  const felt* E = a.rem_E;
+  for (uint32_t k = t; k < m; k += blockDim.x) {
+    const felt wk = fp::pow_u64(a.wd_inv, k);
+    felt p = one(), acc = zero();
+    for (uint32_t i = 0; i < D; i++) {
+      acc = add(acc, mul(E[(i & ((1u << a.logB) - 1)) * m + (i >> a.logB)], p));
+      p = mul(p, wk);
+    }
+    const felt c = mul(mul(acc, a.d_inv), fp::pow_u64(a.rem_off_inv, k));
+    s_c[k] = c;
+    a.rem_out[k] = c;
+  }
+  __syncthreads();
+  uint32_t h[8];
+  hash_felts_block([&](uint32_t i) { return s_c[i]; }, m, h, s_cv);
+  if (t == 0) {
+    uint32_t st[8];
+    for (int i = 0; i < 8; i++) st[i] = a.coin_seed[i];
+    dcoin_reseed(st, h);
+    for (int i = 0; i < 8; i++) { a.coin_seed[i] = st[i]; a.commit_out[i] = h[i]; }
+  }
 }
 
 // multi-segment gather: segment s copies seg[s].count items of seg[s].words
@@ -1924,6 +2022,13 @@ void launch_fri_fold(Prof& prof, hipStream_t s, const felt* E, uint64_t m16, uin
   LAUNCH(prof, "fri_fold16", s, (double)rows * (16 * 16.0 + 16.0),
          hipLaunchKernelGGL(k_fri_fold16, dim3(blocks_for(rows)), dim3(TPB), 0, s, E, rows, logm16, j0, logB, alpha,
                             off_inv, lev, eps_inv, out));
+}
+
+void launch_fri_tail(Prof& prof, hipStream_t s, const FriTailArgs& a) {
+  if (a.nl > FRI_TAIL_MAX || (a.rem_m << a.logB) > 256) abort();
+  for (uint32_t l = 0; l < a.nl; l++)
+    if (a.ly[l].logm16 + a.logB > 7) abort();  // <= 128 rows: one quad per row in 512 threads
+  LAUNCH(prof, "fri_tail", s, 0.0, hipLaunchKernelGGL(k_fri_tail, dim3(1), dim3(512), 0, s, a));
 }
 
 void launch_leaf_hash_shard(Prof& prof, hipStream_t s, int mode, const felt* src, uint64_t n, uint32_t cols,

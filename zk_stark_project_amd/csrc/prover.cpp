@@ -1149,11 +1149,39 @@ int prove_impl(zkp_ctx* ctx, zkp_comm* cm, int air_id, const felt* d_trace, uint
     felt* alphas_d = reinterpret_cast<felt*>(coin_d + 8);
     uint32_t* roots_d = coin_d + 8 + 4 * (size_t)L;
     HIP_CHECK(hipMemcpyAsync(coin_d, dt_seed, 32, hipMemcpyDeviceToDevice, st));  // device transcript
+    // world 1 with a device remainder: the layers of <= 128 rows, their coin
+    // steps and the remainder run as one single-block launch (k_fri_tail)
+    static const bool no_fri_tail = getenv("ZKP_NO_FRI_TAIL") != nullptr;  // A/B switch
+    const bool fuse_tail = R == 1 && o->grinding_factor > 0 && F == 16 && (N >> (4 * L)) <= 256 && !no_fri_tail;
+    FriTailArgs fta{};
     for (uint32_t l = 0; l < L; l++) {
       const uint64_t m16 = m / F;
       if (sh && (m16 >> logR) < 16) replicate(l);
       FriLayer& ly = layers[l];
       ly.E = E; ly.m = m; ly.Bc = Bc; ly.jc = jc; ly.sharded = sh;
+      if (fuse_tail && (m16 << logB) <= 128) {
+        if (fta.nl >= FRI_TAIL_MAX) throw ZkpFail{ZKP_ERR_DEVICE, "FRI tail: too many small layers"};
+        ly.tree.logR = 0;
+        ly.tree.Lr = m16 << logB;
+        ly.tree.nodes = ctx->buf<uint32_t>("ftree_" + std::to_string(l), (size_t)16 * ly.tree.Lr);
+        ly.tree.top.assign(2, {});
+        FriTailLayer& y = fta.ly[fta.nl++];
+        y.E = E;
+        y.nodes = ly.tree.nodes;
+        y.logm16 = ilog2(m16);
+        y.off_inv = inv(off);
+        y.lev = ctx->itws(logN) + ((1ull << (ilog2(D) - 1)) - 1);  // as launch_fri_fold
+        y.out = fe + eo;
+        y.alpha_out = alphas_d + l;
+        y.root_out = roots_d + 8 * (size_t)l;
+        E = fe + eo;
+        eo += (uint64_t)Bc * m16;
+        m = m16;
+        D /= F;
+        off = pow_u64(off, F);
+        continue;
+      }
+      if (fta.nl) throw ZkpFail{ZKP_ERR_DEVICE, "FRI tail: a large layer after a small one"};
       // sharded layers assemble the root on the host (top levels); it is staged back for the coin
       MerkleTail coin{};
       coin.op = MERKLE_TAIL_FRI_COIN;
@@ -1187,6 +1215,7 @@ int prove_impl(zkp_ctx* ctx, zkp_comm* cm, int air_id, const felt* d_trace, uint
     // returns the nonce (the host replays and checks all of it)
     const uint64_t Dlast = (uint64_t)B * m;
     dev_tail = Dlast <= 256 && o->grinding_factor > 0;
+    if (fuse_tail && !dev_tail) throw ZkpFail{ZKP_ERR_DEVICE, "FRI tail fused without a device remainder"};
     // world 1: the whole query tail runs on the device too (grinding to completion,
     // query positions, every opening the batch proofs can need), so the proof has
     // a single host round trip, at its end
@@ -1194,8 +1223,22 @@ int prove_impl(zkp_ctx* ctx, zkp_comm* cm, int air_id, const felt* d_trace, uint
     if (dev_tail) {
       rem_d = ctx->buf<felt>("rem_d", m + 1);
       rcommit_d = ctx->buf<uint32_t>("rem_commit", 8);
-      launch_fri_remainder(pf, st, E, logB, (uint32_t)m, inv(off), inv(root_of_unity(ilog2(Dlast))),
-                           inv(felt_u64(Dlast)), coin_d, rem_d, rcommit_d);
+      if (fuse_tail) {
+        fta.logB = logB;
+        fta.coin_seed = coin_d;
+        fta.eps_inv = deps;
+        fta.rem_E = E;
+        fta.rem_m = (uint32_t)m;
+        fta.rem_off_inv = inv(off);
+        fta.wd_inv = inv(root_of_unity(ilog2(Dlast)));
+        fta.d_inv = inv(felt_u64(Dlast));
+        fta.rem_out = rem_d;
+        fta.commit_out = rcommit_d;
+        launch_fri_tail(pf, st, fta);
+      } else {
+        launch_fri_remainder(pf, st, E, logB, (uint32_t)m, inv(off), inv(root_of_unity(ilog2(Dlast))),
+                             inv(felt_u64(Dlast)), coin_d, rem_d, rcommit_d);
+      }
       HIP_CHECK(hipMemsetAsync(dres, 0xff, 8, st));
       if (dev_query)
         launch_grind_all(pf, st, coin_d, 1, 1ull << 40, o->grinding_factor, dres);

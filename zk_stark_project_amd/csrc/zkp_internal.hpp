@@ -249,6 +249,31 @@ void launch_deep(Prof& prof, hipStream_t s, const DeepArgs& a, felt* out);
 void launch_fri_fold(Prof& prof, hipStream_t s, const felt* E, uint64_t m16, uint32_t Bl, uint32_t j0,
                      uint32_t logB, uint32_t F, const felt* alpha, felt off_inv, const felt* itw, uint32_t logD,
                      const felt* eps_inv_dev, felt* out);
+// the FRI tail in one block (world 1): layers of <= 128 rows (tree, coin step,
+// fold) and the remainder, in order
+constexpr uint32_t FRI_TAIL_MAX = 4;
+struct FriTailLayer {
+  const felt* E;        // layer evaluations, coset-major (B cosets of 16 * 2^logm16)
+  uint32_t* nodes;      // the layer's tree (16 * rows words)
+  uint32_t logm16;
+  felt off_inv;
+  const felt* lev;      // w_D^-r table of the layer's domain
+  felt* out;            // folded evaluations (the next layer)
+  felt* alpha_out;      // device transcript slots
+  uint32_t* root_out;
+};
+struct FriTailArgs {
+  uint32_t nl, logB;
+  FriTailLayer ly[FRI_TAIL_MAX];
+  uint32_t* coin_seed;
+  const felt* eps_inv;
+  const felt* rem_E;    // last layer: rem_m positions per coset
+  uint32_t rem_m;
+  felt rem_off_inv, wd_inv, d_inv;
+  felt* rem_out;
+  uint32_t* commit_out;
+};
+void launch_fri_tail(Prof& prof, hipStream_t s, const FriTailArgs& a);
 // device-side coin step of the FRI loop: seed = merge(seed, root); *alpha_out = draw(); root copied to root_out
 void launch_coin_fri_layer(Prof& prof, hipStream_t s, uint32_t* seed, const uint32_t* root, felt* alpha_out,
                            uint32_t* root_out);
