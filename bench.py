@@ -57,7 +57,7 @@ KERNEL_STAGES = {
     "ntt_dit": ("lde", "comp_lde"), "ntt_dif": ("intt", "comp_intt"), "deep": ("deep",),
     "eval_mimc": ("eval",), "eval_linear": ("eval",),
 }
-PMC_TAGS = ("r02", "r01")  # newest committed PMC summaries first (scripts/profile_round.sh)
+PMC_TAGS = ("r03", "r02_final", "r02", "r01")  # newest committed PMC summaries first (scripts/profile_round.sh)
 
 
 def stage_bytes(w: int, n: int, B: int, ce: int, C: int, rem: int = 7, F: int = 16) -> dict:
@@ -155,6 +155,64 @@ def isa_mix() -> dict:
     return {k.replace("(anonymous namespace)::", "").split("(")[0]: v["slow_frac"] for k, v in d.items()}
 
 
+def host_cpus() -> int:
+    """CPUs this job may use on the host: the cgroup cpu.max quota when one is set
+    (the GPU box gives each job a share of a larger machine), else the scheduler
+    affinity. os.cpu_count() reports the whole machine either way."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota, period = f.read().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, int(int(quota) // int(period))))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
+def c1_leg(ctx) -> dict:
+    """BASELINE configs[0] / SURVEY §8(d) C1: benches/bench_mimc.rs:17-60 restated —
+    mimc_cipher(x, rc, 0) with x, rc = the first two next_u64 of StdRng::from_seed([24; 32])
+    (tests/golden/mimc.json, ChaCha12 restated) and mimc_hash_matrix over the bench's
+    6x9 of 42.0 and 6 of 1.0, timed on one host thread by the C oracle; plus a MiMC-AIR
+    STARK at n = 2^10 (blowup 8, options of C2) on the CPU oracle and on the GPU."""
+    import oracle_ref
+    from zk_stark_project_amd import AIR_MIMC, MimcProver, ProofOptions, helper
+    with open(os.path.join(ROOT, "tests", "golden", "mimc.json")) as f:
+        kat = json.load(f)
+    bc = kat["bench_mimc_cipher"]
+    x, rc = int(bc["x"]), int(bc["rc"])
+    assert oracle_ref.mimc_cipher(x, rc, 0) == int(bc["out"])
+    cipher_s, _ = oracle_ref.time_mimc_cipher(x, rc, 200000)
+    w = [[helper.f64_to_felt(42.0)] * 9] * 6
+    b = [helper.f64_to_felt(1.0)] * 6
+    rcs = helper.get_round_constants()
+    _, d = oracle_ref.time_mimc_hash_matrix(w, b, rcs, 1)
+    assert d == int(kat["mimc_hash_matrix_bench"])
+    hash_s, _ = oracle_ref.time_mimc_hash_matrix(w, b, rcs, 2000)
+    opts = ProofOptions(40, 8, 21)
+    prover = MimcProver(opts, ctx)
+    n = 1 << 10
+    trace = prover.build_trace(42 * 10**6, n)
+    pub = prover.get_pub_inputs(trace).to_elements()
+    pb = b"".join(v.to_bytes(16, "little") for v in pub)
+    t0 = time.perf_counter()
+    cproof, _ = oracle_ref.prove(AIR_MIMC, trace.to_bytes(), 1, n, pb, opts)
+    cpu_ms = (time.perf_counter() - t0) * 1e3
+    ctx.prove(AIR_MIMC, trace.data, pub, opts)  # warm the 2^10 domain tables
+    reps = 20
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        gproof, _ = ctx.prove(AIR_MIMC, trace.data, pub, opts)
+    gpu_ms = (time.perf_counter() - t0) * 1e3 / reps
+    return {"workload": "benches/bench_mimc.rs (BASELINE configs[0]) + MiMC AIR 2^10 STARK, blowup 8",
+            "mimc_cipher_ns": round(cipher_s * 1e9, 1), "mimc_hash_matrix_us": round(hash_s * 1e6, 2),
+            "cipher_inputs": "StdRng::from_seed([24; 32]) next_u64 x2 (tests/golden/mimc.json)",
+            "helpers_on": "C oracle, 1 host thread",
+            "stark_2e10_cpu_ms": round(cpu_ms, 2), "cpu_threads": oracle_ref.lib().oracle_num_threads(),
+            "stark_2e10_gpu_ms": round(gpu_ms, 3), "proof_bytes_identical": cproof == gproof}
+
+
 def host_info():
     model = None
     try:
@@ -165,7 +223,8 @@ def host_info():
                     break
     except OSError:
         pass
-    return {"os_cpu_count": os.cpu_count(), "model": model, "OMP_NUM_THREADS": os.environ.get("OMP_NUM_THREADS")}
+    return {"os_cpu_count": os.cpu_count(), "job_cpus": host_cpus(), "model": model,
+            "OMP_NUM_THREADS": os.environ.get("OMP_NUM_THREADS")}
 
 
 def parse():
@@ -215,6 +274,23 @@ def make_workload(air: str, sharded: bool, log_n, blowup: int, seed_rank: int, c
                 ce=2, C=1, workload=f"GlobalUpdate AIR, {ndev} updates padded to 2^{log_n} rows, w=120 ({cfg})")
 
 
+WATCHDOG_EXIT = 3  # exit status of every rank when the sharded leg hangs
+
+
+def watchdog(done: threading.Event, timeout_s: float, rank: int, on_timeout=None, exit_fn=os._exit):
+    """Ends the process with WATCHDOG_EXIT unless `done` is set within timeout_s: a
+    hung collective must not look like a clean run (rank 0 first prints the
+    headline line it already has, with the error, so the measurement survives)."""
+    if done.wait(timeout_s):
+        return
+    print(json.dumps({"error": f"sharded leg exceeded {timeout_s:.0f} s on rank {rank}"}), file=sys.stderr, flush=True)
+    if on_timeout is not None:
+        on_timeout()
+    sys.stdout.flush()
+    sys.stderr.flush()
+    exit_fn(WATCHDOG_EXIT)
+
+
 def sharded_leg(ctx, rank: int, world: int, dist, local_rank: int, on_timeout=None, timeout_s: float = 120.0):
     """One C4 proof (MiMC 2^22, B = 8) split over all `world` ranks by LDE coset over
     RCCL; timed like the headline (barrier + device sync, max over ranks). Runs after
@@ -225,16 +301,7 @@ def sharded_leg(ctx, rank: int, world: int, dist, local_rank: int, on_timeout=No
     from zk_stark_project_amd.sharded import rccl_group_comm
 
     done = threading.Event()
-
-    def watchdog():
-        if not done.wait(timeout_s):
-            print(json.dumps({"error": f"sharded leg exceeded {timeout_s:.0f} s on rank {rank}"}), file=sys.stderr,
-                  flush=True)
-            if on_timeout is not None:
-                on_timeout()
-            sys.stdout.flush()
-            os._exit(0)
-    threading.Thread(target=watchdog, daemon=True).start()
+    threading.Thread(target=watchdog, args=(done, timeout_s, rank, on_timeout), daemon=True).start()
     wl = make_workload("mimc", True, None, 8, 0, ctx)
     pub = wl["prover"].get_pub_inputs(wl["trace"]).to_elements()
     comm = rccl_group_comm(ctx, rank, world)
@@ -345,13 +412,18 @@ def main():
         comm.close()
     run_sharded = world > 1 and not sharded and not args.no_sharded_leg
     if rank != 0:
+        failed = False
         if run_sharded:  # collective with rank 0's leg below
             try:
                 sharded_leg(ctx, rank, world, dist, local_rank)
-            except Exception:  # noqa: BLE001 — rank 0 reports it
-                pass
+            except Exception as e:  # noqa: BLE001 — rank 0 reports the leg; this rank exits non-zero
+                print(json.dumps({"error": f"sharded leg failed on rank {rank}: {type(e).__name__}: {e}"}),
+                      file=sys.stderr, flush=True)
+                failed = True
         if dist is not None:
             dist.destroy_process_group()
+        if failed:
+            sys.exit(1)
         return
 
     B = opts.blowup_factor
@@ -391,8 +463,14 @@ def main():
     }
 
     cpu = None
+    c1 = None
     if world == 1 and not args.no_cpu_baseline and not sharded:
         import oracle_ref
+        # the whole host share this job may use (cgroup quota / affinity), not an inherited
+        # OMP_NUM_THREADS: the oracle's OpenMP regions run on every CPU available to it
+        oracle_ref.lib().oracle_set_threads(host_cpus())
+        if args.air == "mimc":
+            c1 = c1_leg(ctx)
         tb = trace.to_bytes()
         pb = b"".join(v.to_bytes(16, "little") for v in pub)
         # bounded sample: whole proofs of the same workload until >= 10 s of CPU work (at most 5)
@@ -412,8 +490,9 @@ def main():
             "kind": "port",
             "host": host_info(),
             "sample": f"{count} full proof(s) of the same workload ({wl['workload']}) by the C oracle restating the "
-                      f"winterfell 0.12 CPU path (OpenMP threads = cores), {dt * 1e3:.0f} ms in all; proof bytes "
-                      f"identical to GPU: {same}",
+                      f"winterfell 0.12 CPU path (OpenMP threads = cores = every CPU of this job's host share: "
+                      f"cgroup quota / affinity, of {os.cpu_count()} on the machine), {dt * 1e3:.0f} ms in all; "
+                      f"proof bytes identical to GPU: {same}",
         }
 
     metric = (f"STARK proofs/sec + prove-time ms, MiMC AIR 2^{wl['log_n']}-step trace" if args.air == "mimc"
@@ -443,6 +522,7 @@ def main():
         "sustained": {"proofs": sus_n, "seconds": round(sus_s, 3), "proofs_per_s": round(sus_n / sus_s, 3)},
         "roofline": roofline,
         "cpu_baseline": cpu,
+        "c1": c1,
         "proof_bytes": len(proof),
         "verified_by_oracle": verified,
         "parity": "bit-exact vs the C oracle; parity vs winterfell 0.12 bytes unpinned (DESIGN.md §2)",

@@ -223,6 +223,10 @@ int zkp_session_create(zkp_ctx* ctx, zkp_air_id air, uint32_t width, uint64_t n,
                        uint64_t n_pub, const zkp_proof_options* opts, zkp_session** out);
 /* Releases the session's device buffers (the ctx stays usable). */
 void zkp_session_destroy(zkp_session* s);
+/* The session's shape as the AIR defines it (each pointer nullable): ce = the
+ * constraint-evaluation blowup (zkp_eval_constraints' evals_out holds n*ce values),
+ * num_columns = C composition columns, fri_layers = FRI layers before the remainder. */
+int zkp_session_shape(const zkp_session* s, uint32_t* ce, uint32_t* num_columns, uint32_t* fri_layers);
 /* Host trace (column-major width*n) -> interpolation, coset LDE, row commitment; root out. */
 int zkp_session_trace_lde(zkp_session* s, const zkp_felt* trace_cols, uint8_t root[32]);
 /* Composition coefficients as the caller's channel drew them (ConstraintCompositionCoefficients:

@@ -10,7 +10,9 @@ Provenance of each pin:
                     SURVEY.md F1: p, generator 3, two-adicity 40, root).
   * mimc.json     — src/helper.rs:25-27 (f64_to_felt), :213-233 (mimc_cipher,
                     mimc_hash_matrix), :404-406 (round constants); the bench
-                    inputs of benches/bench_mimc.rs:41-45 (SURVEY.md Appendix D);
+                    inputs of benches/bench_mimc.rs:41-45 and
+                    :22-27 (StdRng = ChaCha12, restated in spec.py and pinned by
+                    the RFC 8439 §2.3.2 ChaCha20 block vector);
                     the builder-defined MiMC AIR trace.
   * ntt.json      — naive O(n^2) interpolation + coset evaluation (DFT definition).
   * merkle.json   — naive MerkleTree::new over hash_elements(row) leaves.
@@ -88,6 +90,11 @@ def main():
             {"x": "7", "rc": "11", "z": "13", "out": str(spec.mimc_cipher(7, 11, 13))},
         ],
         "mimc_hash_matrix_bench": str(spec.mimc_hash_matrix([[42 * 10**6] * 9] * 6, [10**6] * 6, rcs)),
+        # benches/bench_mimc.rs:17-34: x, rc = the first two next_u64 of StdRng::from_seed([24; 32])
+        # (ChaCha12 restated in spec.py, its core pinned by the RFC 8439 block vector)
+        "bench_mimc_cipher": (lambda xr: {"seed_byte": 24, "x": str(xr[0]), "rc": str(xr[1]), "z": "0",
+                                          "out": str(spec.mimc_cipher(xr[0], xr[1], 0))})(
+            spec.stdrng_next_u64(bytes([24] * 32), 2)),
         "mimc_air_trace_x0_42e6_n64": [str(v) for v in trace],
     })
 

@@ -182,3 +182,44 @@ def merkle_root(leaves):
     while len(level) > 1:
         level = [merge(level[2 * i], level[2 * i + 1]) for i in range(len(level) // 2)]
     return level[0]
+
+
+# ---------------------------------------------------------------- ChaCha (rand 0.8 StdRng)
+# StdRng = rand_chacha ChaCha12Rng (rand 0.8, Cargo.lock): state = "expand 32-byte k",
+# key = the 32-byte seed, 64-bit block counter in words 12-13 (from 0), 64-bit stream
+# id 0 in words 14-15; output block = rounds(state) + state, 16 LE u32 words;
+# RngCore::next_u64 reads words (2i, 2i+1) as lo | hi << 32 (rand_core BlockRng).
+def _chacha_block(key: bytes, counter: int, nonce_words, rounds: int):
+    M = 0xFFFFFFFF
+    s = [0x61707865, 0x3320646E, 0x79622D32, 0x6B206574]
+    s += [int.from_bytes(key[4 * i:4 * i + 4], "little") for i in range(8)]
+    s += [counter & M] + list(nonce_words)
+    x = list(s)
+
+    def rotl(v, n):
+        return ((v << n) | (v >> (32 - n))) & M
+
+    def qr(a, b, c, d):
+        x[a] = (x[a] + x[b]) & M; x[d] = rotl(x[d] ^ x[a], 16)
+        x[c] = (x[c] + x[d]) & M; x[b] = rotl(x[b] ^ x[c], 12)
+        x[a] = (x[a] + x[b]) & M; x[d] = rotl(x[d] ^ x[a], 8)
+        x[c] = (x[c] + x[d]) & M; x[b] = rotl(x[b] ^ x[c], 7)
+    for _ in range(rounds // 2):
+        qr(0, 4, 8, 12); qr(1, 5, 9, 13); qr(2, 6, 10, 14); qr(3, 7, 11, 15)
+        qr(0, 5, 10, 15); qr(1, 6, 11, 12); qr(2, 7, 8, 13); qr(3, 4, 9, 14)
+    return [(a + b) & M for a, b in zip(x, s)]
+
+
+def chacha20_block_rfc8439(key: bytes, counter: int, nonce: bytes):
+    """RFC 8439 §2.3 layout (32-bit counter, 96-bit nonce): the published test vector pins the core."""
+    return _chacha_block(key, counter, [int.from_bytes(nonce[4 * i:4 * i + 4], "little") for i in range(3)], 20)
+
+
+def stdrng_next_u64(seed: bytes, count: int):
+    """First `count` next_u64() of rand 0.8 `StdRng::from_seed(seed)` (ChaCha12, counter 0, stream 0)."""
+    words = []
+    blk = 0
+    while len(words) < 2 * count:
+        words += _chacha_block(seed, blk, [0, 0, 0], 12)  # block counter < 2^32 here: high word 0
+        blk += 1
+    return [words[2 * i] | (words[2 * i + 1] << 32) for i in range(count)]

@@ -72,6 +72,20 @@ def lib():
         L.oracle_grind.restype = ctypes.c_uint64
         L.oracle_grind.argtypes = [ctypes.c_char_p, ctypes.c_uint32]
         L.oracle_num_threads.restype = ctypes.c_int
+        L.oracle_set_threads.argtypes = [ctypes.c_int]
+        L.oracle_set_threads.restype = None
+        L.oracle_mimc_hash_matrix.argtypes = [ctypes.c_char_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_char_p,
+                                              ctypes.c_char_p, ctypes.c_uint32, ctypes.c_char_p]
+        L.oracle_mimc_hash_matrix.restype = None
+        L.oracle_gu_trace.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_uint64,
+                                      ctypes.c_char_p, ctypes.c_uint64, ctypes.c_char_p, ctypes.c_char_p]
+        L.oracle_gu_trace.restype = ctypes.c_int
+        L.oracle_time_mimc_cipher.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_uint64, ctypes.c_char_p]
+        L.oracle_time_mimc_cipher.restype = ctypes.c_double
+        L.oracle_time_mimc_hash_matrix.argtypes = [ctypes.c_char_p, ctypes.c_uint32, ctypes.c_uint32,
+                                                   ctypes.c_char_p, ctypes.c_char_p, ctypes.c_uint32,
+                                                   ctypes.c_uint64, ctypes.c_char_p]
+        L.oracle_time_mimc_hash_matrix.restype = ctypes.c_double
         _lib = L
     return _lib
 
@@ -199,3 +213,43 @@ def prove_stages(air_id: int, trace_cols: bytes, width: int, n: int, pub: bytes,
            "ood": bufs["ood"].raw, "deep_coeffs": bufs["deep_coeffs"].raw,
            "alphas": bufs["alphas"].raw[:16 * sd.n_layers], "remainder": bufs["remainder"].raw[:16 * sd.n_remainder]}
     return proof, res
+
+
+def mimc_hash_matrix(w, b, rc) -> int:
+    """helper.rs:222-233 on the oracle (C)."""
+    out = ctypes.create_string_buffer(16)
+    wb = b"".join(fb(v) for row in w for v in row)
+    lib().oracle_mimc_hash_matrix(wb, len(w), len(w[0]) if w else 0, b"".join(fb(v) for v in b),
+                                  b"".join(fb(v) for v in rc), len(rc), out)
+    return int.from_bytes(out.raw, "little")
+
+
+def gu_trace(raw, blinding, local, k: int, n: int):
+    """GlobalUpdateProver trace (src/aggregation/prover.rs:98-160) on the oracle:
+    -> (column-major 120 x n trace bytes, final state ints). raw/blinding: 60 ints,
+    local: ndev lists of 60 ints (flattened w then b)."""
+    ndev = len(local)
+    out = ctypes.create_string_buffer(120 * n * 16)
+    fin = ctypes.create_string_buffer(60 * 16)
+    rc = lib().oracle_gu_trace(b"".join(fb(v) for v in raw), b"".join(fb(v) for v in blinding),
+                               b"".join(fb(v) for row in local for v in row) or b"\0" * 16, ndev, fb(k), n,
+                               out, fin)
+    if rc != 0:
+        raise ValueError("oracle_gu_trace: n < ndev + 2")
+    return out.raw, [int.from_bytes(fin.raw[16 * i:16 * i + 16], "little") for i in range(60)]
+
+
+def time_mimc_cipher(x: int, rc: int, iters: int):
+    """C1 mimc_cipher timing (one host thread): (seconds per call, chained output)."""
+    out = ctypes.create_string_buffer(16)
+    sec = lib().oracle_time_mimc_cipher(fb(x), fb(rc), iters, out)
+    return sec, int.from_bytes(out.raw, "little")
+
+
+def time_mimc_hash_matrix(w, b, rc, iters: int):
+    """C1 mimc_hash_matrix timing (one host thread): (seconds per call, last digest)."""
+    out = ctypes.create_string_buffer(16)
+    sec = lib().oracle_time_mimc_hash_matrix(b"".join(fb(v) for row in w for v in row), len(w), len(w[0]),
+                                             b"".join(fb(v) for v in b), b"".join(fb(v) for v in rc), len(rc),
+                                             iters, out)
+    return sec, int.from_bytes(out.raw, "little")

@@ -59,7 +59,8 @@ def _rank(rank, world, port, kind, q, fail_rank):
             q.put((rank, "error", repr(e)))
         comm.close()
         ctx.close()
-        dist.destroy_process_group()
+        if dist.is_initialized():  # a failed proof already tore the group down (gloo_abort)
+            dist.destroy_process_group()
     except Exception:  # noqa: BLE001
         q.put((rank, "crash", traceback.format_exc()))
 

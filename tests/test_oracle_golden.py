@@ -121,6 +121,22 @@ def test_helper_mirror_matches_golden():
     b = [helper.f64_to_felt(1.0)] * 6
     assert helper.mimc_hash_matrix(w, b, helper.get_round_constants()) == int(g["mimc_hash_matrix_bench"])
     assert int(g["mimc_hash_matrix_bench"]) == 29677690899009456259734863514471282405
+    assert O.mimc_hash_matrix(w, b, helper.get_round_constants()) == int(g["mimc_hash_matrix_bench"])
+
+
+def test_bench_mimc_inputs_stdrng():
+    """benches/bench_mimc.rs:17-34 draws x, rc from StdRng::from_seed([24; 32]) (ChaCha12):
+    the restatement's core reproduces the RFC 8439 §2.3.2 ChaCha20 block, and the
+    fixture's inputs/output match it, the helper mirror and the oracle."""
+    from zk_stark_project_amd import helper
+    blk = spec.chacha20_block_rfc8439(bytes(range(32)), 1, bytes.fromhex("000000090000004a00000000"))
+    assert b"".join(w.to_bytes(4, "little") for w in blk).hex() == (
+        "10f1e7e4d13b5915500fdd1fa32071c4c7d1f4c733c068030422aa9ac3d46c4e"
+        "d2826446079faa0914c2d705d98b02a2b5129cd1de164eb9cbd083e8a2503c4e")
+    c = load("mimc.json")["bench_mimc_cipher"]
+    x, rc = spec.stdrng_next_u64(bytes([24] * 32), 2)
+    assert (str(x), str(rc)) == (c["x"], c["rc"])
+    assert helper.mimc_cipher(x, rc, 0) == int(c["out"]) == O.mimc_cipher(x, rc, 0)
 
 
 def test_reference_helper_semantics():
@@ -238,6 +254,23 @@ def test_global_update_trace_semantics():
     e = pub.to_elements()
     assert len(e) == 123 and e[120] == p.k and e[122] == 7
     assert e[60:120] == last[:60] and all(v == 0 for v in last[60:])
+
+
+@pytest.mark.parametrize("ndev,n", [(0, 8), (1, 8), (6, 16), (64, 1 << 10), (300, 512)])
+def test_oracle_gu_trace_matches_host_mirror(ndev, n):
+    """The oracle's restatement of GlobalUpdateProver::build_trace (prover.rs:98-160, C)
+    and the product's host mirror (prover.py) agree byte for byte, final state included."""
+    from zk_stark_project_amd import ProofOptions
+    from zk_stark_project_amd.prover import _flatten
+    p = gu(ndev, n, ndev + n, ProofOptions.reference())
+    raw = _flatten(p.raw_global_w, p.raw_global_b)
+    local = [_flatten(w, b) for w, b in zip(p.local_w, p.local_b)]
+    tb, fin = O.gu_trace(raw, p.blinding, local, p.k, n)
+    assert tb == p.build_trace().to_bytes()
+    assert fin == p.compute_iterative_trace_augmented()[ndev + 1][:60]
+    if ndev:  # too short a trace is refused
+        with pytest.raises(ValueError):
+            O.gu_trace(raw, p.blinding, local, p.k, ndev + 1)
 
 
 def test_oracle_global_update_roundtrip():

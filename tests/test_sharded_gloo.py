@@ -96,3 +96,64 @@ def test_two_rank_gloo_caller_transport():
         want = bytes((s * 100 + r * 10 + i) % 256 for s in range(world) for i in range(block))
         assert recv == want
         assert gat == bytes((s * 7 + i) % 256 for s in range(world) for i in range(block))
+
+
+def _abort_worker(rank, world, port, out):
+    """Rank 1 takes part in one collective, then fails and calls the transport's
+    abort (what zkp_prove_sharded does on error); rank 0's next collective must
+    fail promptly instead of blocking until the group timeout."""
+    import ctypes
+    import datetime
+    import time
+
+    import numpy as np
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=120))
+    from zk_stark_project_amd import _native, sharded
+    a2a, ag = sharded.gloo_transport(world)
+    captured = {}
+
+    def fake_create(w, r, tp, outp):
+        captured["t"] = ctypes.cast(tp, ctypes.POINTER(_native.HostTransport))[0]
+        outp._obj.value = 1
+        return 0
+
+    class FakeLib:
+        zkp_comm_host_create = staticmethod(fake_create)
+
+        def zkp_comm_destroy(self, p):
+            pass
+    real_load = _native.load
+    _native.load = lambda: FakeLib()
+    try:
+        comm = _native.host_comm(rank, world, a2a, ag, abort=sharded.gloo_abort())
+    finally:
+        _native.load = real_load
+    t = captured["t"]
+    mine = np.full(16, rank, dtype=np.uint8)
+    gat = np.zeros(world * 16, dtype=np.uint8)
+    rc1 = t.all_gather(None, mine.ctypes.data, gat.ctypes.data, 16)
+    t0 = time.monotonic()
+    if rank == 1:
+        t.abort(None)  # the failing rank releases its peers
+        rc2 = None
+    else:
+        rc2 = t.all_gather(None, mine.ctypes.data, gat.ctypes.data, 16)
+    out[rank] = (rc1, rc2, time.monotonic() - t0, dist.is_initialized())
+    comm.ptr = ctypes.c_void_p()
+    if dist.is_initialized():
+        dist.destroy_process_group()
+
+
+def test_gloo_abort_releases_peer_after_first_collective():
+    world = 2
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_abort_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    rc1_0, rc2_0, dt0, _ = out[0]
+    rc1_1, _, _, alive1 = out[1]
+    assert rc1_0 == 0 and rc1_1 == 0      # the first collective ran on both ranks
+    assert not alive1                      # the abort tore down the failing rank's group
+    assert rc2_0 == 1                      # the peer's next collective failed ...
+    assert dt0 < 60                        # ... long before the 120 s group timeout

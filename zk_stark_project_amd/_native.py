@@ -75,6 +75,7 @@ EXPORTED = [
     "zkp_verify", "zkp_build_global_update_trace", "zkp_set_profiling_kernel",
     "zkp_session_create", "zkp_session_destroy", "zkp_session_trace_lde", "zkp_eval_constraints",
     "zkp_composition_commit", "zkp_ood_frame", "zkp_deep_fri", "zkp_query", "zkp_comm_host_create",
+    "zkp_session_shape",
 ]
 
 # zkp_host_transport callbacks (include/zkp.h)
@@ -168,6 +169,7 @@ def load():
         L.zkp_session_create.argtypes = [vp, i32, u32, u64, vp, u64, popt, ctypes.POINTER(vp)]
         L.zkp_session_destroy.argtypes = [vp]
         L.zkp_session_destroy.restype = None
+        L.zkp_session_shape.argtypes = [vp, ctypes.POINTER(u32), ctypes.POINTER(u32), ctypes.POINTER(u32)]
         L.zkp_session_trace_lde.argtypes = [vp, vp, ctypes.c_char_p]
         L.zkp_eval_constraints.argtypes = [vp, vp, u32, vp]
         L.zkp_composition_commit.argtypes = [vp, vp, ctypes.c_char_p, ctypes.POINTER(u32)]
@@ -466,7 +468,6 @@ class Session:
 
     def __init__(self, ctx: "Context", air_id: int, width: int, n: int, pub, options: ProofOptions):
         self.ctx, self.lib, self.width, self.n = ctx, ctx.lib, width, n
-        self.ce = 8 if air_id == 1 else 2  # constraint-evaluation blowup: MiMC degree 7, linear AIRs degree 1
         self.ptr = ctypes.c_void_p()
         self._pub = _felts(pub) if len(pub) else None
         self._opts = options.to_c()
@@ -474,6 +475,11 @@ class Session:
                                                self._pub.ctypes.data if self._pub is not None else None,
                                                len(pub), ctypes.byref(self._opts), ctypes.byref(self.ptr)),
                    "zkp_session_create")
+        # the AIR's own shape (not re-derived here): evals_out holds n*ce values
+        ce, nc, nl = ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_uint32()
+        ctx._check(self.lib.zkp_session_shape(self.ptr, ctypes.byref(ce), ctypes.byref(nc), ctypes.byref(nl)),
+                   "zkp_session_shape")
+        self.ce, self.fri_layers = ce.value, nl.value
         self.num_columns = None
 
     def close(self):

@@ -5,6 +5,7 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <mutex>
 
 using kc::static_for;
 using kc::rev_bits;
@@ -527,8 +528,15 @@ void launch_ntt(Prof& prof, hipStream_t s, const NttBatch& b, uint32_t logn, boo
     return;
   }
   uint32_t npass = (logn + KMAX - 1) / KMAX;
-  static bool attr_set = false;
-  if (!attr_set) {
+  // the dynamic-LDS attributes are per device: set them once for each device this
+  // process launches on (threads of an in-process group drive different devices)
+  static std::mutex attr_mu;
+  static uint64_t attr_devs = 0;
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  {
+  std::lock_guard<std::mutex> attr_lock(attr_mu);
+  if (!(attr_devs >> (dev & 63) & 1)) {
     size_t maxb = (size_t)(1u << LOGE) * sizeof(felt);
     const void* fns[] = {
         (const void*)k_ntt8<true, 256, 5, false>,  (const void*)k_ntt8<true, 256, 6, false>,
@@ -545,7 +553,8 @@ void launch_ntt(Prof& prof, hipStream_t s, const NttBatch& b, uint32_t logn, boo
                         (const void*)k_ntt8<true, 512, 10, false>, (const void*)k_ntt8<false, 512, 10, false>,
                         (const void*)k_ntt8<true, 512, 10, true>,  (const void*)k_ntt8<false, 512, 10, true>};
     for (const void* f : k9) (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 4096 * 16);
-    attr_set = true;
+    attr_devs |= 1ull << (dev & 63);
+  }
   }
   // pass sizes: prefer multiples of 3 (whole radix-8 rounds), largest pass last
   uint32_t Ks[4] = {0, 0, 0, 0};

@@ -1895,6 +1895,14 @@ void zkp_session_destroy(zkp_session* s) {
   delete s;
 }
 
+int zkp_session_shape(const zkp_session* s, uint32_t* ce, uint32_t* num_columns, uint32_t* fri_layers) {
+  if (!s) return ZKP_ERR_ARGUMENT;
+  if (ce) *ce = s->ce;
+  if (num_columns) *num_columns = s->C;
+  if (fri_layers) *fri_layers = s->L;
+  return ZKP_OK;
+}
+
 int zkp_session_trace_lde(zkp_session* s, const zkp_felt* trace_cols, uint8_t root[32]) {
   return session_guard(s, [&] {
     if (!trace_cols || !root) return (int)ZKP_ERR_ARGUMENT;

@@ -97,7 +97,22 @@ def gloo_transport(world: int, group=None):
     return all_to_all, all_gather
 
 
+def gloo_abort(group=None):
+    """The transport's abort (zkp_comm abort, called by a rank whose proof fails):
+    tearing down this rank's process group closes its gloo connections, so peers
+    blocked in a collective with it fail at once instead of waiting out the
+    group timeout (30 min by default; callers should still init with a short one)."""
+    import torch.distributed as dist
+
+    def abort():
+        if dist.is_initialized():
+            dist.destroy_process_group(group)
+    return abort
+
+
 def gloo_group_comm(rank: int, world: int, group=None):
-    """`zkp_comm` whose collectives run over torch.distributed (initialised with gloo)."""
+    """`zkp_comm` whose collectives run over torch.distributed (initialised with gloo).
+    On a failed proof the library calls the abort: this rank's group is destroyed
+    (check `torch.distributed.is_initialized()` before destroying it again)."""
     a2a, ag = gloo_transport(world, group)
-    return _native.host_comm(rank, world, a2a, ag)
+    return _native.host_comm(rank, world, a2a, ag, abort=gloo_abort(group))
