@@ -53,22 +53,41 @@ __global__ void k_build_coset_scale(felt* S, uint32_t logn, uint32_t B, const fe
 // recv: slices [pl0, pl0 + nR) (bit-reversed positions p) of the CE cosets'
 // Gentleman-Sande inverse NTTs (position p holds n * V_u[rev(p)]); blk[u] =
 // receive block of CE coset u. Si[u*n + p] = (g w_M^u)^-rev(p) turns them into
-// n * U_u[rev(p)], and n * c_m[rev(p)] = sum_u n U_u * coefs[u*C + m] with
-// coefs = w_ce^-um * g^-mn / ce. out[m*nR + pl]: the bit-reversed, n-scaled
-// coefficient layout of the LDE input (directly the columns when nR = n).
+// n * U_u[rev(p)], and n * c_m[rev(p)] = (sum_u n U_u w_ce^-um) * g^-mn / ce: a
+// CE-point inverse DFT per position (radix-2 in registers, compile-time indices)
+// and one scale per kept column. consts = [g^-mn / ce for m < C | w_ce^-k for k < CE/2].
+// out[m*nR + pl]: the bit-reversed, n-scaled coefficient layout of the LDE input
+// (directly the columns when nR = n).
+template <int CE>
 __global__ __launch_bounds__(TPB) void k_comp_dft(const felt* __restrict__ recv, const uint32_t* __restrict__ blk,
-                                                  const felt* __restrict__ Si, const felt* __restrict__ coefs,
-                                                  uint32_t ce, uint32_t C, uint32_t logn, uint64_t p0, uint64_t nR,
+                                                  const felt* __restrict__ Si, const felt* __restrict__ consts,
+                                                  uint32_t C, uint32_t logn, uint64_t p0, uint64_t nR,
                                                   felt* __restrict__ out) {
   const uint64_t pl = blockIdx.x * (uint64_t)TPB + threadIdx.x;
   if (pl >= nR) return;
-  felt U[16];
-  for (uint32_t u = 0; u < ce; u++) U[u] = mul(recv[blk[u] * nR + pl], Si[((uint64_t)u << logn) + p0 + pl]);
-  for (uint32_t m = 0; m < C; m++) {
-    felt acc = zero();
-    for (uint32_t u = 0; u < ce; u++) acc = add(acc, mul(U[u], coefs[u * C + m]));
-    out[m * nR + pl] = acc;
-  }
+  felt x[CE];
+  static_for<0, CE>([&](auto uu) {
+    constexpr int u = decltype(uu)::value;
+    x[u] = mul(recv[blk[u] * nR + pl], Si[((uint64_t)u << logn) + p0 + pl]);
+  });
+  const felt* winv = consts + C;
+  // Gentleman-Sande: natural in, bit-reversed out; x[rev(m)] = sum_u U_u w_ce^-um
+  static_for<0, kc::ilog2_const(CE)>([&](auto ss) {
+    constexpr int len = CE >> decltype(ss)::value, h = len / 2;
+    static_for<0, CE / len>([&](auto bb) {
+      constexpr int b0 = decltype(bb)::value * len;
+      static_for<0, h>([&](auto jj) {
+        constexpr int j = decltype(jj)::value;
+        const felt u = x[b0 + j], v = x[b0 + j + h];
+        x[b0 + j] = add(u, v);
+        x[b0 + j + h] = j == 0 ? sub(u, v) : mul(sub(u, v), winv[j * (CE / len)]);
+      });
+    });
+  });
+  static_for<0, CE>([&](auto mm) {
+    constexpr int m = decltype(mm)::value;
+    if ((uint32_t)m < C) out[m * nR + pl] = mul(x[kc::rev_const(m, kc::ilog2_const(CE))], consts[m]);
+  });
 }
 
 // coefficient-dependent constants of the constraint evaluation kernels, from cc:
@@ -420,20 +439,27 @@ __global__ __launch_bounds__(TPB) void k_eval_bitrev(const felt* __restrict__ ar
     l = 3;
     m = TPB;
   } else {  // smaller blocks: per = E / TPB consecutive elements per thread (or one)
+    // (E < 2048: per <= 4; compile-time register indices, guarded by the runtime per)
     const uint32_t per = E >= TPB ? E / TPB : 1;
-    felt v0[8], v1[8];
-    for (uint32_t i = 0; i < per; i++) {
-      felt x = (t * per + i < E) ? src[t * per + i] : zero();
+    felt v0[4], v1[4];
+    static_for<0, 4>([&](auto ii) {
+      constexpr uint32_t i = decltype(ii)::value;
+      const felt x = (i < per && t * per + i < E) ? src[t * per + i] : zero();
       v0[i] = x;
       v1[i] = x;
-    }
-    for (uint32_t w = per; w > 1; w >>= 1, l++) {
-      const felt m0 = pw0[logn - 1 - l], m1 = pw1[logn - 1 - l];
-      for (uint32_t i = 0; i < w / 2; i++) {
-        v0[i] = add(v0[2 * i], mul(m0, v0[2 * i + 1]));
-        v1[i] = add(v1[2 * i], mul(m1, v1[2 * i + 1]));
+    });
+    static_for<0, 2>([&](auto lv) {
+      constexpr uint32_t w = 4u >> decltype(lv)::value;  // 4, then 2 values reduced per level
+      if (w <= per) {
+        const felt m0 = pw0[logn - 1 - l], m1 = pw1[logn - 1 - l];
+        static_for<0, (int)(w / 2)>([&](auto ii) {
+          constexpr uint32_t i = decltype(ii)::value;
+          v0[i] = add(v0[2 * i], mul(m0, v0[2 * i + 1]));
+          v1[i] = add(v1[2 * i], mul(m1, v1[2 * i + 1]));
+        });
+        l++;
       }
-    }
+    });
     s0[t] = v0[0];
     s1[t] = v1[0];
     m = E >= TPB ? TPB : E;
@@ -539,6 +565,31 @@ __global__ __launch_bounds__(TPB) void k_deep(DeepArgs a, const felt* __restrict
   static_for<0, EVAL_CH>([&](auto k) {
     const uint64_t q = EVAL_POINT(k);
     if (q < N) out[q] = mul(num[k], den[k]);
+  });
+}
+
+// Coefficient-form DEEP, step 1 (wide traces): the gamma-combination of the w
+// trace polynomials in coefficient form, out[p] = sum_c gamma_c * coef_c[p]
+// (bit-reversed, n-scaled like its inputs). LIN_CH positions per thread, TPB
+// apart; column-outer so each column's loads are in flight together. Its coset
+// LDE then replaces w column reads per LDE point of the pointwise k_deep by one.
+__global__ __launch_bounds__(TPB) void k_deep_lincomb(const felt* __restrict__ coef, uint32_t w, uint64_t n,
+                                                      const felt* __restrict__ gamma, felt* __restrict__ out) {
+  felt acc[LIN_CH];
+  uint64_t p[LIN_CH];
+  static_for<0, LIN_CH>([&](auto k) {
+    p[k] = LIN_POINT(k) < n ? LIN_POINT(k) : 0;
+    acc[k] = zero();
+  });
+  for (uint32_t c = 0; c < w; c++) {
+    const felt g = gamma[c];
+    const felt* col = coef + (uint64_t)c * n;
+    felt v[LIN_CH];
+    static_for<0, LIN_CH>([&](auto k) { v[k] = col[p[k]]; });
+    static_for<0, LIN_CH>([&](auto k) { acc[k] = add(acc[k], mul(g, v[k])); });
+  }
+  static_for<0, LIN_CH>([&](auto k) {
+    if (LIN_POINT(k) < n) out[LIN_POINT(k)] = acc[k];
   });
 }
 
@@ -771,6 +822,13 @@ void launch_deep_denominators(Prof& prof, hipStream_t s, const PointMap& m, uint
   launch_den_inverse(prof, s, m, count, zero(), zero(), 1, binv, zz, pw);
 }
 
+void launch_deep_lincomb(Prof& prof, hipStream_t s, const felt* coef, uint32_t w, uint64_t n, const felt* gamma,
+                         felt* out) {
+  LAUNCH(prof, "deep_lincomb", s, (double)(w + 1) * n * 16.0,
+         hipLaunchKernelGGL(k_deep_lincomb, dim3(blocks_for((n + LIN_CH - 1) / LIN_CH)), dim3(TPB), 0, s, coef, w, n,
+                            gamma, out));
+}
+
 void launch_deep(Prof& prof, hipStream_t s, const DeepArgs& a, felt* out) {
   uint64_t N = 1ull << (a.logn + a.logBl);
   LAUNCH(prof, "deep", s, (double)N * ((a.w + a.C) * 16.0 + 16.0),
@@ -778,10 +836,20 @@ void launch_deep(Prof& prof, hipStream_t s, const DeepArgs& a, felt* out) {
 }
 
 void launch_comp_dft(Prof& prof, hipStream_t s, const felt* recv, const uint32_t* blk, const felt* Si,
-                     const felt* coefs, uint32_t ce, uint32_t C, uint32_t logn, uint64_t p0, uint64_t nR, felt* out) {
-  LAUNCH(prof, "comp_dft", s, (double)nR * (2 * ce + C) * 16.0,
-         hipLaunchKernelGGL(k_comp_dft, dim3(blocks_for(nR)), dim3(TPB), 0, s, recv, blk, Si, coefs, ce, C, logn, p0,
-                            nR, out));
+                     const felt* consts, uint32_t ce, uint32_t C, uint32_t logn, uint64_t p0, uint64_t nR, felt* out) {
+  const double bytes = (double)nR * (2 * ce + C) * 16.0;
+  const dim3 g(blocks_for(nR));
+  switch (ce) {
+    case 2: LAUNCH(prof, "comp_dft", s, bytes, hipLaunchKernelGGL(k_comp_dft<2>, g, dim3(TPB), 0, s, recv, blk, Si,
+                                                                   consts, C, logn, p0, nR, out)); break;
+    case 4: LAUNCH(prof, "comp_dft", s, bytes, hipLaunchKernelGGL(k_comp_dft<4>, g, dim3(TPB), 0, s, recv, blk, Si,
+                                                                   consts, C, logn, p0, nR, out)); break;
+    case 8: LAUNCH(prof, "comp_dft", s, bytes, hipLaunchKernelGGL(k_comp_dft<8>, g, dim3(TPB), 0, s, recv, blk, Si,
+                                                                   consts, C, logn, p0, nR, out)); break;
+    case 16: LAUNCH(prof, "comp_dft", s, bytes, hipLaunchKernelGGL(k_comp_dft<16>, g, dim3(TPB), 0, s, recv, blk,
+                                                                    Si, consts, C, logn, p0, nR, out)); break;
+    default: abort();  // the prover admits ce <= 16 (ZKP_ERR_UNSUPPORTED_AIR otherwise)
+  }
 }
 
 void launch_gather_multi(Prof& prof, hipStream_t s, const GatherSeg* segs, uint32_t nseg, uint64_t max_count,

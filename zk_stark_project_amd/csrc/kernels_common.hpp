@@ -34,6 +34,9 @@ __device__ __forceinline__ void static_for(F&& f) {
   }
 }
 
+constexpr int ilog2_const(int v) { return v <= 1 ? 0 : 1 + ilog2_const(v / 2); }
+constexpr int rev_const(int x, int bits) { return bits == 0 ? 0 : ((x & 1) << (bits - 1)) | rev_const(x >> 1, bits - 1); }
+
 inline uint32_t ilog2_u64(uint64_t v) {
   uint32_t l = 0;
   while ((1ull << l) < v) l++;

@@ -188,7 +188,7 @@ __device__ __forceinline__ void merge8(const uint32_t l[8], const uint32_t r[8],
   b3::compress(out, m, 0, 64, b3::CHUNK_START | b3::CHUNK_END | b3::ROOT);
 }
 
-__device__ void merkle_tail_op(const MerkleTail& tl, const uint32_t* root);
+__device__ __forceinline__ void merkle_tail_op(const MerkleTail& tl, const uint32_t* root);
 
 // QUAD (MODE 1 with 16-felt rows only): 64 leaves per block, each hashed by a
 // quad of lanes (compress_quad), so a small FRI layer's leaf stage is four
@@ -455,7 +455,7 @@ __device__ __forceinline__ felt dcoin_draw(const uint32_t s[8], uint64_t* ctr) {
 // draw `ncoef` coefficients into out (whole block; the coin state s was just
 // reseeded, counter 0): Linear = ncoef draws (parallel candidates, sequential redo
 // on a rejection), Algebraic = powers of one draw, Horner = the powers reversed
-__device__ void dcoin_draw_coeffs_block(const uint32_t s[8], uint32_t method, uint32_t ncoef, felt* out,
+__device__ __forceinline__ void dcoin_draw_coeffs_block(const uint32_t s[8], uint32_t method, uint32_t ncoef, felt* out,
                                         felt* s_alpha, int* s_rej) {
   if (threadIdx.x == 0) {
     *s_rej = 0;
@@ -489,7 +489,7 @@ __device__ void dcoin_draw_coeffs_block(const uint32_t s[8], uint32_t method, ui
 // (64 felts) on thread c, then the chunk tree (left subtree = largest power of
 // two) on thread 0 with the incremental stack. nf <= 64 * 32.
 template <typename Get>
-__device__ void hash_felts_block(Get get, uint32_t nf, uint32_t out[8], uint32_t (*s_cv)[8]) {
+__device__ __forceinline__ void hash_felts_block(Get get, uint32_t nf, uint32_t out[8], uint32_t (*s_cv)[8]) {
   const uint32_t nch = nf ? (nf + 63) / 64 : 1;
   for (uint32_t c = threadIdx.x; c < nch; c += blockDim.x) {
     uint32_t cv[8];
@@ -502,15 +502,20 @@ __device__ void hash_felts_block(Get get, uint32_t nf, uint32_t out[8], uint32_t
     if (nch == 1) {
       for (int i = 0; i < 8; i++) out[i] = s_cv[0][i];
     } else {
-      uint32_t st[6][8];
+      // the incremental chunk-tree stack lives in s_cv itself (LDS, so no
+      // scratch): after chunk c the stack holds popcount(c + 1) <= c + 1
+      // entries, at indices below the next chunk still to be read
+      uint32_t (*st)[8] = s_cv;
       int top = 0;
       for (uint32_t c = 0; c + 1 < nch; c++) {
         uint32_t cv[8];
         for (int i = 0; i < 8; i++) cv[i] = s_cv[c][i];
         uint64_t total = c + 1;
         while ((total & 1) == 0) {
-          uint32_t p[8];
-          b3::parent(st[--top], cv, false, p);
+          uint32_t l[8], p[8];
+          --top;
+          for (int i = 0; i < 8; i++) l[i] = st[top][i];
+          b3::parent(l, cv, false, p);
           for (int i = 0; i < 8; i++) cv[i] = p[i];
           total >>= 1;
         }
@@ -520,9 +525,10 @@ __device__ void hash_felts_block(Get get, uint32_t nf, uint32_t out[8], uint32_t
       uint32_t cv[8];
       for (int i = 0; i < 8; i++) cv[i] = s_cv[nch - 1][i];
       while (top > 0) {
-        uint32_t p[8];
+        uint32_t l[8], p[8];
         top--;
-        b3::parent(st[top], cv, top == 0, p);
+        for (int i = 0; i < 8; i++) l[i] = st[top][i];
+        b3::parent(l, cv, top == 0, p);
         for (int i = 0; i < 8; i++) cv[i] = p[i];
       }
       for (int i = 0; i < 8; i++) out[i] = cv[i];
@@ -589,7 +595,7 @@ __global__ __launch_bounds__(64) void k_dt_deep_coeffs(uint32_t* __restrict__ se
 // (ConstraintCompositionCoefficients::draw: Linear = n draws, Algebraic = powers
 // of one draw, Horner = the powers reversed). One block; Linear draws run in
 // parallel with a sequential redo if any candidate was rejected.
-__device__ void dt_draw_coeffs_block(uint32_t* __restrict__ seed, const uint32_t* __restrict__ root, uint32_t method,
+__device__ __forceinline__ void dt_draw_coeffs_block(uint32_t* __restrict__ seed, const uint32_t* __restrict__ root, uint32_t method,
                                      uint32_t ncoef, felt* __restrict__ cc) {
   __shared__ uint32_t s[8];
   __shared__ felt s_alpha;
@@ -613,7 +619,7 @@ __global__ __launch_bounds__(TPB) void k_dt_draw_coeffs(uint32_t* __restrict__ s
 
 // reseed with the constraint root, draw z; zz = (z, z*w_n); pw tables
 // pw[l] = z^(2^l), pw[logn + l] = (z w_n)^(2^l) for the OOD evaluation
-__device__ void dt_draw_z_block(uint32_t* __restrict__ seed, const uint32_t* __restrict__ root, felt wn, uint32_t logn,
+__device__ __forceinline__ void dt_draw_z_block(uint32_t* __restrict__ seed, const uint32_t* __restrict__ root, felt wn, uint32_t logn,
                                 felt* __restrict__ zz, felt* __restrict__ pw) {
   __shared__ felt s_z;
   if (threadIdx.x == 0) {
@@ -642,12 +648,12 @@ __global__ void k_dt_draw_z(uint32_t* __restrict__ seed, const uint32_t* __restr
   dt_draw_z_block(seed, root, wn, logn, zz, pw);
 }
 
-__device__ void coin_fri_step(uint32_t* __restrict__ seed, const uint32_t* root, felt* __restrict__ alpha_out,
+__device__ __forceinline__ void coin_fri_step(uint32_t* __restrict__ seed, const uint32_t* root, felt* __restrict__ alpha_out,
                               uint32_t* __restrict__ root_out);
 
 // what the last block of a finished Merkle tree does with its root (all threads
 // of the block call it; root = nodes + 8, written by this block)
-__device__ void merkle_tail_op(const MerkleTail& tl, const uint32_t* root) {
+__device__ __forceinline__ void merkle_tail_op(const MerkleTail& tl, const uint32_t* root) {
   if (tl.op == MERKLE_TAIL_FRI_COIN) {
     if (threadIdx.x == 0) {
       uint32_t r[8];
@@ -663,7 +669,7 @@ __device__ void merkle_tail_op(const MerkleTail& tl, const uint32_t* root) {
 
 // FRI commit-loop Fiat-Shamir step (one thread): seed <- BLAKE3(seed || root),
 // alpha = first draw < p; root copied to root_out
-__device__ void coin_fri_step(uint32_t* __restrict__ seed, const uint32_t* root, felt* __restrict__ alpha_out,
+__device__ __forceinline__ void coin_fri_step(uint32_t* __restrict__ seed, const uint32_t* root, felt* __restrict__ alpha_out,
                               uint32_t* __restrict__ root_out) {
   uint32_t m[16], s[8];
   for (int i = 0; i < 8; i++) { m[i] = seed[i]; m[8 + i] = root[i]; root_out[i] = root[i]; }

@@ -546,6 +546,50 @@ void constraint_eval(zkp_ctx* ctx, const AirDesc& air, uint32_t logn, uint32_t l
   }
 }
 
+// constants of k_comp_dft: [g^-mn / ce for m < C | w_ce^-k for k < ce/2]
+std::vector<felt> comp_dft_consts(uint64_t n, uint32_t logce, uint32_t C) {
+  const uint32_t ce = 1u << logce;
+  std::vector<felt> dc((size_t)C + ce / 2);
+  const felt g = felt_u64(3), ce_inv = inv(felt_u64(ce)), gn_inv = inv(pow_u64(g, n)),
+             wce_inv = inv(root_of_unity(logce));
+  for (uint32_t m = 0; m < C; m++) dc[m] = mul(pow_u64(gn_inv, m), ce_inv);
+  for (uint32_t k = 0; k < ce / 2; k++) dc[C + k] = pow_u64(wce_inv, k);
+  return dc;
+}
+
+// DEEP composition evaluations over the rank's cosets [j0, j0 + Bl) (coset-major).
+// Narrow traces: pointwise k_deep over every trace and composition column's LDE.
+// Wide traces (w >= DEEP_COEF_MIN_W): winterfell's own dataflow
+// — the gamma-combination of the trace polynomials in coefficient form
+// (k_deep_lincomb over `coef`, read once), its coset LDE, then k_deep over that one
+// column and the composition columns with coefficients [1 | delta]: w column reads
+// per LDE point become one (C3: 8.2 GB -> ~1 GB per proof). Same field values.
+constexpr uint32_t DEEP_COEF_MIN_W = 16;
+void deep_evaluations(zkp_ctx* ctx, hipStream_t st, DeepArgs da, const felt* coef, uint64_t n, const felt* Sj0,
+                      uint32_t logN, felt* out) {
+  static const bool pointwise_only = getenv("ZKP_DEEP_POINTWISE") != nullptr;  // A/B switch
+  if (da.w < DEEP_COEF_MIN_W || pointwise_only) {
+    launch_deep(ctx->prof, st, da, out);
+    return;
+  }
+  const uint32_t Bl = 1u << da.logBl;
+  felt* acomb = ctx->buf<felt>("deep_acoef", n);
+  launch_deep_lincomb(ctx->prof, st, coef, da.w, n, da.gamma, acomb);
+  felt* alde = ctx->buf<felt>("deep_alde", (size_t)Bl * n);
+  NttBatch lb{acomb, alde, Sj0, n, n, Bl, Bl, Bl};
+  launch_ntt(ctx->prof, st, lb, da.logn, true, ctx->tws(logN), logN);
+  felt* g1 = ctx->buf<felt>("deep_g1", (size_t)da.C + 1);  // [1 | delta_0 .. delta_{C-1}]
+  if (!ctx->have_cached("deep_g1")) {
+    const felt unit = one();
+    ctx->upload(g1, &unit, 16);
+  }
+  HIP_CHECK(hipMemcpyAsync(g1 + 1, da.gamma + da.w, (size_t)da.C * 16, hipMemcpyDeviceToDevice, st));
+  da.w = 1;
+  da.tlde = alde;
+  da.gamma = g1;
+  launch_deep(ctx->prof, st, da, out);
+}
+
 // one FRI layer as the prover holds it: coset-major evaluations of the cosets
 // [jc, jc + Bc) (m positions each), and its (possibly sharded) Merkle tree
 struct FriLayer {
@@ -1012,14 +1056,10 @@ int prove_impl(zkp_ctx* ctx, zkp_comm* cm, int air_id, const felt* d_trace, uint
     // (shape-only: cached per (n, ce, C, R, celmax))
     const std::string dkey = "comp_dft_" + std::to_string(logn) + "_" + std::to_string(logce) + "_" +
                              std::to_string(C) + "_" + std::to_string(R) + "_" + std::to_string(celmax);
-    felt* dcoefs = ctx->buf<felt>(dkey + "_coefs", (size_t)ce * C);
+    felt* dcoefs = ctx->buf<felt>(dkey + "_coefs", (size_t)C + ce / 2);
     uint32_t* dblk = ctx->buf<uint32_t>(dkey + "_blk", ce);
     if (!ctx->have_cached(dkey)) {
-      std::vector<felt> dc((size_t)ce * C);
-      felt wce_inv = inv(root_of_unity(logce)), ce_inv = inv(felt_u64(ce)), gn_inv = inv(pow_u64(g, n));
-      for (uint32_t u = 0; u < ce; u++)
-        for (uint32_t m = 0; m < C; m++)
-          dc[(size_t)u * C + m] = mul(mul(pow_u64(wce_inv, (uint64_t)u * m), pow_u64(gn_inv, m)), ce_inv);
+      const std::vector<felt> dc = comp_dft_consts(n, logce, C);
       std::vector<uint32_t> blk(ce);
       for (uint32_t u = 0; u < ce; u++) {
         uint32_t s = ce_owner(u);
@@ -1096,7 +1136,7 @@ int prove_impl(zkp_ctx* ctx, zkp_comm* cm, int air_id, const felt* d_trace, uint
     da.pm = deep_pm;
     da.binv = deep_binv;
     HIP_CHECK(hipStreamWaitEvent(st, ctx->ev_join, 0));
-    launch_deep(pf, st, da, deep);
+    deep_evaluations(ctx, st, da, coef, n, Sj0, logN, deep);
   }
   ctx->stage_end("4_deep_launch");
 
@@ -1980,15 +2020,10 @@ int zkp_composition_commit(zkp_session* s, const zkp_felt* evals, uint8_t root[3
     launch_ntt(pf, st, ib, s->logn, false, ctx->itws(s->logN), s->logN);
     const std::string dkey = "comp_dft_" + std::to_string(s->logn) + "_" + std::to_string(s->logce) + "_" +
                              std::to_string(C) + "_1_" + std::to_string(ce);
-    felt* dcoefs = ctx->buf<felt>(dkey + "_coefs", (size_t)ce * C);
+    felt* dcoefs = ctx->buf<felt>(dkey + "_coefs", (size_t)C + ce / 2);
     uint32_t* dblk = ctx->buf<uint32_t>(dkey + "_blk", ce);
     if (!ctx->have_cached(dkey)) {  // world 1: blk[u] = u (same table as zkp_prove's)
-      std::vector<felt> dc((size_t)ce * C);
-      const felt g = felt_u64(3);
-      felt wce_inv = inv(root_of_unity(s->logce)), ce_inv = inv(felt_u64(ce)), gn_inv = inv(pow_u64(g, n));
-      for (uint32_t u = 0; u < ce; u++)
-        for (uint32_t m = 0; m < C; m++)
-          dc[(size_t)u * C + m] = mul(mul(pow_u64(wce_inv, (uint64_t)u * m), pow_u64(gn_inv, m)), ce_inv);
+      const std::vector<felt> dc = comp_dft_consts(n, s->logce, C);
       std::vector<uint32_t> blk(ce);
       for (uint32_t u = 0; u < ce; u++) blk[u] = u;
       ctx->upload(dcoefs, dc.data(), dc.size() * 16);
@@ -2069,7 +2104,7 @@ int zkp_deep_fri(zkp_session* s, const zkp_felt* deep_coeffs, zkp_fri_channel ch
     da.tlde = s->get("tlde"); da.clde = s->get("clde"); da.gamma = dgam; da.dk = dk; da.g = g;
     da.pm = pm;
     da.binv = binv;
-    launch_deep(pf, st, da, deep);
+    deep_evaluations(ctx, st, da, s->get("coef"), n, ctx->S(s->logn, s->logB), s->logN, deep);
     // FriProver::build_layers: commit each layer, the caller's channel returns alpha, fold
     s->layers.assign(s->L + 1, FriLayer{});
     uint64_t tot = 0, D = s->N;

@@ -216,9 +216,10 @@ void launch_eval_linear(Prof& prof, hipStream_t s, const EvalCommon& c, const Li
                         felt* comp);
 
 // composition polynomial from CE-coset interpolations (see kernels.hip): for the
-// bit-reversed positions [p0, p0 + nR), n * c_m = sum_u Si_u * W_u * coefs[u][m]
+// bit-reversed positions [p0, p0 + nR), n * c_m = (sum_u Si_u * W_u * w_ce^-um) * g^-mn / ce;
+// consts = [g^-mn / ce for m < C | w_ce^-k for k < ce/2] (ce in {2, 4, 8, 16})
 void launch_comp_dft(Prof& prof, hipStream_t s, const felt* recv, const uint32_t* blk, const felt* Si,
-                     const felt* coefs, uint32_t ce, uint32_t C, uint32_t logn, uint64_t p0, uint64_t nR, felt* out);
+                     const felt* consts, uint32_t ce, uint32_t C, uint32_t logn, uint64_t p0, uint64_t nR, felt* out);
 
 // OOD evaluation of bit-reversed arrays (arrays contiguous, stride n) at x0 and x1
 // partial[(a * nblocks + b) * 2 + {0,1}] ; pw0/pw1 = x^(2^l) tables (logn entries, device)
@@ -243,6 +244,11 @@ struct DeepArgs {
 void launch_deep_denominators(Prof& prof, hipStream_t s, const PointMap& m, uint64_t count, const felt* zz,
                               const felt* pw, felt* binv);
 void launch_deep(Prof& prof, hipStream_t s, const DeepArgs& a, felt* out);
+// coefficient-form DEEP for wide traces (winterfell combines the trace polynomials
+// before extending): out[p] = sum_{c < w} gamma[c] * coef[c*n + p]
+// over the bit-reversed, n-scaled coefficient columns -> one combined column (same layout)
+void launch_deep_lincomb(Prof& prof, hipStream_t s, const felt* coef, uint32_t w, uint64_t n, const felt* gamma,
+                         felt* out);
 
 // FRI fold-by-F (F = 16) over coset-major evaluations of the cosets [j0, j0+Bl)
 // (16*m16 positions each): natural row r = j + B*t', x_r = off * w_D^r; alpha read from device
