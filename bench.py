@@ -357,8 +357,18 @@ def main():
         from zk_stark_project_amd.sharded import rccl_group_comm
         comm = rccl_group_comm(ctx, rank, world) if world > 1 else _native.local_group(1)[0]
 
-        def prove_once():  # host trace -> proof (uploads included)
-            return ctx.prove_sharded(comm, air_id, host_trace, pub, opts)
+        if args.air == "agg":
+            # C5: each rank builds the GlobalUpdate trace in its own HBM from the
+            # device updates (zkp_build_global_update_trace, prover.rs:98-160), so
+            # no rank uploads the 2 GiB trace; the step = trace build + proof
+            d_built = ctx.alloc(host_trace.nbytes)
+
+            def prove_once():
+                wl["prover"].build_trace_device(ctx, d_out=d_built)
+                return ctx.prove_sharded(comm, air_id, d_built, pub, opts, shape=(width, n))
+        else:
+            def prove_once():  # host trace -> proof (each rank uploads its row slice; all-gather)
+                return ctx.prove_sharded(comm, air_id, host_trace, pub, opts)
 
         def prove_dev():
             return ctx.prove_sharded(comm, air_id, d_trace, pub, opts, shape=(width, n))
@@ -516,7 +526,9 @@ def main():
                    "trace_length": n, "trace_width": width, "blowup": B, "num_queries": 40, "grinding": 21,
                    "fri_folding": 16, "fri_remainder_max_degree": 7,
                    "parallelism": f"coset-sharded{world} (RCCL)" if sharded else f"replicas{world}",
-                   "step": "zkp_prove: host trace (pageable) -> proof bytes, PCIe upload included"},
+                   "step": ("GlobalUpdate trace built on each rank's device from the updates + zkp_prove_sharded"
+                            if sharded and args.air == "agg" else
+                            "zkp_prove: host trace (pageable) -> proof bytes, PCIe upload included")},
         "device_resident_ms": round(el_dev / args.steps * 1e3, 3),
         "first_proof_ms": round(first_ms, 3),
         "sustained": {"proofs": sus_n, "seconds": round(sus_s, 3), "proofs_per_s": round(sus_n / sus_s, 3)},

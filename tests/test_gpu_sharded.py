@@ -140,3 +140,33 @@ def test_global_update_c5_sharded(ctx, rank_ctxs, world):
     check_all_equal(res, single)
     assert O.verify(AIR_GLOBAL_UPDATE, single, to_bytes(pub), opts) == 0
     _native.verify(AIR_GLOBAL_UPDATE, single, pub, opts)
+    # the bench's C5 step: every rank builds the trace in its own HBM from the updates
+    d = p.build_trace_device(ctx)
+    try:
+        res_dev = prove_local_group(world, AIR_GLOBAL_UPDATE, d, pub, opts, contexts=rank_ctxs[:world],
+                                    shape=(120, 1 << 20))
+    finally:
+        ctx.free(d)
+    check_all_equal(res_dev, single)
+
+
+@pytest.mark.slow
+@pytest.mark.timeout(600)
+def test_global_update_c5_oracle_bytes(rank_ctxs):
+    """C5 shape against the ORACLE: the world-2 sharded proof's
+    bytes equal the oracle's full proof at 2^20 x 120, blowup 16 (the oracle needs
+    ~32 GiB of host memory and tens of seconds on the box's cores; skipped when the
+    host has less than 64 GiB)."""
+    import os
+    mem = os.sysconf("SC_PAGE_SIZE") * os.sysconf("SC_PHYS_PAGES")
+    if mem < (64 << 30):
+        pytest.skip(f"host has {mem >> 30} GiB; the C5 oracle needs ~40 GiB")
+    opts = ProofOptions.reference()
+    p = gu_prover(256, 1 << 20, opts, seed=5)
+    trace = p.build_trace()
+    pub = p.get_pub_inputs(trace).to_elements()
+    res = prove_local_group(2, AIR_GLOBAL_UPDATE, trace.data, pub, opts, contexts=rank_ctxs[:2])
+    ref, tr = O.prove(AIR_GLOBAL_UPDATE, trace.to_bytes(), 120, 1 << 20, to_bytes(pub), opts)
+    assert bytes(res[0][1].trace_root) == bytes(tr.trace_root), "C5 trace root differs from the oracle"
+    assert bytes(res[0][1].constraint_root) == bytes(tr.constraint_root), "C5 constraint root differs"
+    check_all_equal(res, ref)

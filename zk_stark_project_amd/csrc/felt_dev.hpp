@@ -11,105 +11,113 @@
 #include <stdint.h>
 // included from felt.hpp inside the device compilation pass only
 
+// ZKP_ASM_VOLATILE (tuning experiment): volatile asm keeps the source order of
+// the carry chains (the interleaving below) instead of the machine scheduler's
+#ifdef ZKP_ASM_VOLATILE
+#define ZKP_ASM asm volatile
+#else
+#define ZKP_ASM asm
+#endif
+
 namespace fpd {
 
 // ---- 32-bit carry-chain primitives (carry masks in SGPR pairs)
 __device__ __forceinline__ uint32_t add_co(uint32_t a, uint32_t b, uint64_t& co) {
   uint32_t r;
-  asm("v_add_co_u32_e64 %0, %1, %2, %3" : "=v"(r), "=s"(co) : "v"(a), "v"(b));
+  ZKP_ASM("v_add_co_u32_e64 %0, %1, %2, %3" : "=v"(r), "=s"(co) : "v"(a), "v"(b));
   return r;
 }
 __device__ __forceinline__ uint32_t addc_co(uint32_t a, uint32_t b, uint64_t ci, uint64_t& co) {
   uint32_t r;
-  asm("v_addc_co_u32_e64 %0, %1, %2, %3, %4" : "=v"(r), "=s"(co) : "v"(a), "v"(b), "s"(ci));
+  ZKP_ASM("v_addc_co_u32_e64 %0, %1, %2, %3, %4" : "=v"(r), "=s"(co) : "v"(a), "v"(b), "s"(ci));
   return r;
 }
 __device__ __forceinline__ uint32_t addc(uint32_t a, uint32_t b, uint64_t ci) {
   uint32_t r;
   uint64_t dead;
-  asm("v_addc_co_u32_e64 %0, %1, %2, %3, %4" : "=v"(r), "=s"(dead) : "v"(a), "v"(b), "s"(ci));
+  ZKP_ASM("v_addc_co_u32_e64 %0, %1, %2, %3, %4" : "=v"(r), "=s"(dead) : "v"(a), "v"(b), "s"(ci));
   return r;
 }
 __device__ __forceinline__ uint32_t sub_co(uint32_t a, uint32_t b, uint64_t& bo) {
   uint32_t r;
-  asm("v_sub_co_u32_e64 %0, %1, %2, %3" : "=v"(r), "=s"(bo) : "v"(a), "v"(b));
+  ZKP_ASM("v_sub_co_u32_e64 %0, %1, %2, %3" : "=v"(r), "=s"(bo) : "v"(a), "v"(b));
   return r;
 }
 __device__ __forceinline__ uint32_t subb_co(uint32_t a, uint32_t b, uint64_t bi, uint64_t& bo) {
   uint32_t r;
-  asm("v_subb_co_u32_e64 %0, %1, %2, %3, %4" : "=v"(r), "=s"(bo) : "v"(a), "v"(b), "s"(bi));
+  ZKP_ASM("v_subb_co_u32_e64 %0, %1, %2, %3, %4" : "=v"(r), "=s"(bo) : "v"(a), "v"(b), "s"(bi));
   return r;
 }
 __device__ __forceinline__ uint32_t subb(uint32_t a, uint32_t b, uint64_t bi) {
   uint32_t r;
   uint64_t dead;
-  asm("v_subb_co_u32_e64 %0, %1, %2, %3, %4" : "=v"(r), "=s"(dead) : "v"(a), "v"(b), "s"(bi));
+  ZKP_ASM("v_subb_co_u32_e64 %0, %1, %2, %3, %4" : "=v"(r), "=s"(dead) : "v"(a), "v"(b), "s"(bi));
   return r;
 }
 // d = a*b + c (64-bit), carry-out of the 64-bit add in co
 __device__ __forceinline__ uint64_t mad_co(uint32_t a, uint32_t b, uint64_t c, uint64_t& co) {
   uint64_t d;
-  asm("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=v"(d), "=s"(co) : "v"(a), "v"(b), "v"(c));
+  ZKP_ASM("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=v"(d), "=s"(co) : "v"(a), "v"(b), "v"(c));
   return d;
 }
 __device__ __forceinline__ uint64_t mad(uint32_t a, uint32_t b, uint64_t c) {
   uint64_t d, dead;
-  asm("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=v"(d), "=s"(dead) : "v"(a), "v"(b), "v"(c));
+  ZKP_ASM("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=v"(d), "=s"(dead) : "v"(a), "v"(b), "v"(c));
   return d;
 }
 // the same with an inline-constant operand (-1 = 0xffffffff or 0), which
 // needs no VGPR (VOP3 takes inline constants; 0x2cff is not one)
 __device__ __forceinline__ uint32_t add_co_m1(uint32_t a, uint64_t& co) {
   uint32_t r;
-  asm("v_add_co_u32_e64 %0, %1, %2, -1" : "=v"(r), "=s"(co) : "v"(a));
+  ZKP_ASM("v_add_co_u32_e64 %0, %1, %2, -1" : "=v"(r), "=s"(co) : "v"(a));
   return r;
 }
 __device__ __forceinline__ uint32_t addc_co_0(uint32_t a, uint64_t ci, uint64_t& co) {
   uint32_t r;
-  asm("v_addc_co_u32_e64 %0, %1, %2, 0, %3" : "=v"(r), "=s"(co) : "v"(a), "s"(ci));
+  ZKP_ASM("v_addc_co_u32_e64 %0, %1, %2, 0, %3" : "=v"(r), "=s"(co) : "v"(a), "s"(ci));
   return r;
 }
 __device__ __forceinline__ uint32_t addc_0(uint32_t a, uint64_t ci) {
   uint32_t r;
   uint64_t dead;
-  asm("v_addc_co_u32_e64 %0, %1, %2, 0, %3" : "=v"(r), "=s"(dead) : "v"(a), "s"(ci));
+  ZKP_ASM("v_addc_co_u32_e64 %0, %1, %2, 0, %3" : "=v"(r), "=s"(dead) : "v"(a), "s"(ci));
   return r;
 }
 __device__ __forceinline__ uint32_t carry_0(uint64_t ci) {  // 0 + 0 + carry
   uint32_t r;
   uint64_t dead;
-  asm("v_addc_co_u32_e64 %0, %1, 0, 0, %2" : "=v"(r), "=s"(dead) : "s"(ci));
+  ZKP_ASM("v_addc_co_u32_e64 %0, %1, 0, 0, %2" : "=v"(r), "=s"(dead) : "s"(ci));
   return r;
 }
 __device__ __forceinline__ uint32_t subb_co_0(uint32_t a, uint64_t bi, uint64_t& bo) {
   uint32_t r;
-  asm("v_subb_co_u32_e64 %0, %1, %2, 0, %3" : "=v"(r), "=s"(bo) : "v"(a), "s"(bi));
+  ZKP_ASM("v_subb_co_u32_e64 %0, %1, %2, 0, %3" : "=v"(r), "=s"(bo) : "v"(a), "s"(bi));
   return r;
 }
 __device__ __forceinline__ uint32_t subb_0(uint32_t a, uint64_t bi) {
   uint32_t r;
   uint64_t dead;
-  asm("v_subb_co_u32_e64 %0, %1, %2, 0, %3" : "=v"(r), "=s"(dead) : "v"(a), "s"(bi));
+  ZKP_ASM("v_subb_co_u32_e64 %0, %1, %2, 0, %3" : "=v"(r), "=s"(dead) : "v"(a), "s"(bi));
   return r;
 }
 __device__ __forceinline__ uint32_t sel_0_m1(uint64_t m) {  // m ? 0xffffffff : 0
   uint32_t r;
-  asm("v_cndmask_b32_e64 %0, 0, -1, %1" : "=v"(r) : "s"(m));
+  ZKP_ASM("v_cndmask_b32_e64 %0, 0, -1, %1" : "=v"(r) : "s"(m));
   return r;
 }
 __device__ __forceinline__ uint64_t mul_wide(uint32_t a, uint32_t b) {  // a*b + 0 (inline)
   uint64_t d, dead;
-  asm("v_mad_u64_u32 %0, %1, %2, %3, 0" : "=v"(d), "=s"(dead) : "v"(a), "v"(b));
+  ZKP_ASM("v_mad_u64_u32 %0, %1, %2, %3, 0" : "=v"(d), "=s"(dead) : "v"(a), "v"(b));
   return d;
 }
 __device__ __forceinline__ uint64_t or_mask(uint64_t a, uint64_t b) {
   uint64_t r;
-  asm("s_or_b64 %0, %1, %2" : "=s"(r) : "s"(a), "s"(b) : "scc");
+  ZKP_ASM("s_or_b64 %0, %1, %2" : "=s"(r) : "s"(a), "s"(b) : "scc");
   return r;
 }
 __device__ __forceinline__ uint32_t sel(uint32_t f, uint32_t t, uint64_t m) {  // m ? t : f
   uint32_t r;
-  asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(f), "v"(t), "s"(m));
+  ZKP_ASM("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(f), "v"(t), "s"(m));
   return r;
 }
 
@@ -251,7 +259,7 @@ __device__ __forceinline__ felt reduce(const uint32_t r[8]) {
   uint32_t z3 = subb_co_0(y3, b, b);
   // net bit 128 = top - borrow (>= 0 overall); set when top & !borrow
   uint64_t k;
-  asm("s_andn2_b64 %0, %1, %2" : "=s"(k) : "s"(top), "s"(b) : "scc");
+  ZKP_ASM("s_andn2_b64 %0, %1, %2" : "=s"(k) : "s"(top), "s"(b) : "scc");
   return canon_from(z0, z1, z2, z3, k);
 }
 
@@ -354,8 +362,8 @@ __device__ __forceinline__ void reduce_x2(const uint32_t r[8], const uint32_t s[
   uint32_t z3 = subb_co_0(y3, b, b);
   uint32_t Z3 = subb_co_0(Y3, f, f);
   uint64_t k1, k2;
-  asm("s_andn2_b64 %0, %1, %2" : "=s"(k1) : "s"(c), "s"(b) : "scc");
-  asm("s_andn2_b64 %0, %1, %2" : "=s"(k2) : "s"(e), "s"(f) : "scc");
+  ZKP_ASM("s_andn2_b64 %0, %1, %2" : "=s"(k1) : "s"(c), "s"(b) : "scc");
+  ZKP_ASM("s_andn2_b64 %0, %1, %2" : "=s"(k2) : "s"(e), "s"(f) : "scc");
   // canonicalize both (interleaved)
   uint64_t g1, g2;
   uint32_t t0 = add_co_m1(z0, g1);
@@ -404,4 +412,163 @@ __device__ __forceinline__ void addsub(felt a, felt b, felt& sum, felt& diff) {
   diff = join(e0, e1, e2, e3);
 }
 
+
+// N independent products with every step issued for all N chains before the
+// next step: each SGPR carry is consumed N instructions after it is produced,
+// so with N >= 3 no s_nop is needed for the carry hazard (N = 2 leaves one
+// wait state per step, which the compiler fills with s_nop 0: ~25% of the
+// NTT's instructions were such nops). Loops have constant trip counts and are
+// fully unrolled, so every array below lives in registers.
+template <int N>
+__device__ __forceinline__ void mul_xn(const felt* a, const felt* b, felt* out) {
+  L4 x[N], y[N];
+  uint32_t r[N][8];
+  uint64_t acc[N], c[N];
+  uint32_t ov[N];
+#pragma unroll
+  for (int k = 0; k < N; k++) { x[k] = split(a[k]); y[k] = split(b[k]); }
+#pragma unroll
+  for (int k = 0; k < N; k++) acc[k] = mul_wide(x[k].w0, y[k].w0);
+#pragma unroll
+  for (int k = 0; k < N; k++) { r[k][0] = (uint32_t)acc[k]; acc[k] >>= 32; }
+  auto wi = [](const L4& v, int i) { return i == 0 ? v.w0 : i == 1 ? v.w1 : i == 2 ? v.w2 : v.w3; };
+  // column col = i + j over the pairs (i, j); first pair starts the overflow word
+#define ZKP_XN_COL(col, ...)                                                            \
+  {                                                                                     \
+    constexpr int pairs[][2] = {__VA_ARGS__};                                           \
+    constexpr int np = sizeof(pairs) / sizeof(pairs[0]);                                \
+    _Pragma("unroll") for (int q = 0; q < np; q++) {                                    \
+      _Pragma("unroll") for (int k = 0; k < N; k++)                                     \
+        acc[k] = mad_co(wi(x[k], pairs[q][0]), wi(y[k], pairs[q][1]), acc[k], c[k]);    \
+      _Pragma("unroll") for (int k = 0; k < N; k++)                                     \
+        ov[k] = q == 0 ? carry_0(c[k]) : addc_0(ov[k], c[k]);                           \
+    }                                                                                   \
+    _Pragma("unroll") for (int k = 0; k < N; k++) {                                     \
+      r[k][col] = (uint32_t)acc[k];                                                     \
+      acc[k] = (acc[k] >> 32) | ((uint64_t)ov[k] << 32);                                \
+    }                                                                                   \
+  }
+  ZKP_XN_COL(1, {0, 1}, {1, 0})
+  ZKP_XN_COL(2, {0, 2}, {1, 1}, {2, 0})
+  ZKP_XN_COL(3, {0, 3}, {1, 2}, {2, 1}, {3, 0})
+  ZKP_XN_COL(4, {1, 3}, {2, 2}, {3, 1})
+  ZKP_XN_COL(5, {2, 3}, {3, 2})
+#undef ZKP_XN_COL
+#pragma unroll
+  for (int k = 0; k < N; k++) acc[k] = mad(x[k].w3, y[k].w3, acc[k]);  // column 6 cannot overflow
+#pragma unroll
+  for (int k = 0; k < N; k++) { r[k][6] = (uint32_t)acc[k]; r[k][7] = (uint32_t)(acc[k] >> 32); }
+  // reduction (as reduce(), N chains interleaved step by step)
+  const uint32_t K = 0x2d00u;
+  uint32_t q0[N], q1[N], q2[N], q3[N], q4[N];
+#pragma unroll
+  for (int k = 0; k < N; k++) {
+    uint64_t t = mul_wide(r[k][4], K);
+    q0[k] = (uint32_t)t;
+    t = mad(r[k][5], K, t >> 32);
+    q1[k] = (uint32_t)t;
+    t = mad(r[k][6], K, t >> 32);
+    q2[k] = (uint32_t)t;
+    t = mad(r[k][7], K, t >> 32);
+    q3[k] = (uint32_t)t;
+    q4[k] = (uint32_t)(t >> 32);
+  }
+  uint64_t cc[N], bb[N];
+  uint32_t s1[N], s2[N], s3[N], s4[N], s5[N], x0[N], x1[N], x2[N], x3[N], x4[N], x5[N];
+#pragma unroll
+  for (int k = 0; k < N; k++) s1[k] = add_co(r[k][1], q0[k], cc[k]);
+#pragma unroll
+  for (int k = 0; k < N; k++) x0[k] = sub_co(r[k][0], r[k][4], bb[k]);
+#pragma unroll
+  for (int k = 0; k < N; k++) s2[k] = addc_co(r[k][2], q1[k], cc[k], cc[k]);
+#pragma unroll
+  for (int k = 0; k < N; k++) x1[k] = subb_co(s1[k], r[k][5], bb[k], bb[k]);
+#pragma unroll
+  for (int k = 0; k < N; k++) s3[k] = addc_co(r[k][3], q2[k], cc[k], cc[k]);
+#pragma unroll
+  for (int k = 0; k < N; k++) x2[k] = subb_co(s2[k], r[k][6], bb[k], bb[k]);
+#pragma unroll
+  for (int k = 0; k < N; k++) s4[k] = addc_co_0(q3[k], cc[k], cc[k]);
+#pragma unroll
+  for (int k = 0; k < N; k++) x3[k] = subb_co(s3[k], r[k][7], bb[k], bb[k]);
+#pragma unroll
+  for (int k = 0; k < N; k++) s5[k] = addc_0(q4[k], cc[k]);
+#pragma unroll
+  for (int k = 0; k < N; k++) x4[k] = subb_co_0(s4[k], bb[k], bb[k]);
+#pragma unroll
+  for (int k = 0; k < N; k++) x5[k] = subb_0(s5[k], bb[k]);
+  uint32_t u0[N], u1[N], y1[N], y2[N], y3[N], z0[N], z1[N], z2[N], z3[N];
+#pragma unroll
+  for (int k = 0; k < N; k++) {
+    uint64_t u = mul_wide(x4[k], K);
+    u0[k] = (uint32_t)u;
+    u1[k] = (uint32_t)(u >> 32) + x5[k] * K;
+  }
+#pragma unroll
+  for (int k = 0; k < N; k++) y1[k] = add_co(x1[k], u0[k], cc[k]);
+#pragma unroll
+  for (int k = 0; k < N; k++) z0[k] = sub_co(x0[k], x4[k], bb[k]);
+#pragma unroll
+  for (int k = 0; k < N; k++) y2[k] = addc_co(x2[k], u1[k], cc[k], cc[k]);
+#pragma unroll
+  for (int k = 0; k < N; k++) z1[k] = subb_co(y1[k], x5[k], bb[k], bb[k]);
+#pragma unroll
+  for (int k = 0; k < N; k++) y3[k] = addc_co_0(x3[k], cc[k], cc[k]);
+#pragma unroll
+  for (int k = 0; k < N; k++) z2[k] = subb_co_0(y2[k], bb[k], bb[k]);
+#pragma unroll
+  for (int k = 0; k < N; k++) z3[k] = subb_co_0(y3[k], bb[k], bb[k]);
+  uint64_t kk[N], g[N];
+#pragma unroll
+  for (int k = 0; k < N; k++) asm("s_andn2_b64 %0, %1, %2" : "=s"(kk[k]) : "s"(cc[k]), "s"(bb[k]) : "scc");
+  uint32_t t0[N], t1[N], t2[N], t3[N];
+#pragma unroll
+  for (int k = 0; k < N; k++) t0[k] = add_co_m1(z0[k], g[k]);
+#pragma unroll
+  for (int k = 0; k < N; k++) t1[k] = addc_co(z1[k], C1, g[k], g[k]);
+#pragma unroll
+  for (int k = 0; k < N; k++) t2[k] = addc_co_0(z2[k], g[k], g[k]);
+#pragma unroll
+  for (int k = 0; k < N; k++) t3[k] = addc_co_0(z3[k], g[k], g[k]);
+#pragma unroll
+  for (int k = 0; k < N; k++) {
+    const uint64_t m = or_mask(kk[k], g[k]);
+    out[k] = join(sel(z0[k], t0[k], m), sel(z1[k], t1[k], m), sel(z2[k], t2[k], m), sel(z3[k], t3[k], m));
+  }
+}
+
+// N independent (x + y, x - y) pairs, step-interleaved like mul_xn
+template <int N>
+__device__ __forceinline__ void addsub_xn(const felt* a, const felt* b, felt* sum, felt* diff) {
+  L4 x[N], y[N];
+  uint64_t c[N], bw[N], g[N], b2[N];
+  uint32_t s0[N], s1[N], s2[N], s3[N], d0[N], d1[N], d2[N], d3[N];
+#pragma unroll
+  for (int k = 0; k < N; k++) { x[k] = split(a[k]); y[k] = split(b[k]); }
+#pragma unroll
+  for (int k = 0; k < N; k++) { s0[k] = add_co(x[k].w0, y[k].w0, c[k]); d0[k] = sub_co(x[k].w0, y[k].w0, bw[k]); }
+#pragma unroll
+  for (int k = 0; k < N; k++) { s1[k] = addc_co(x[k].w1, y[k].w1, c[k], c[k]); d1[k] = subb_co(x[k].w1, y[k].w1, bw[k], bw[k]); }
+#pragma unroll
+  for (int k = 0; k < N; k++) { s2[k] = addc_co(x[k].w2, y[k].w2, c[k], c[k]); d2[k] = subb_co(x[k].w2, y[k].w2, bw[k], bw[k]); }
+#pragma unroll
+  for (int k = 0; k < N; k++) { s3[k] = addc_co(x[k].w3, y[k].w3, c[k], c[k]); d3[k] = subb_co(x[k].w3, y[k].w3, bw[k], bw[k]); }
+  uint32_t m0[N], m1[N], t0[N], t1[N], t2[N], t3[N], e0[N], e1[N], e2[N], e3[N];
+#pragma unroll
+  for (int k = 0; k < N; k++) { m0[k] = sel_0_m1(bw[k]); m1[k] = sel(0u, C1, bw[k]); }
+#pragma unroll
+  for (int k = 0; k < N; k++) { t0[k] = add_co_m1(s0[k], g[k]); e0[k] = sub_co(d0[k], m0[k], b2[k]); }
+#pragma unroll
+  for (int k = 0; k < N; k++) { t1[k] = addc_co(s1[k], C1, g[k], g[k]); e1[k] = subb_co(d1[k], m1[k], b2[k], b2[k]); }
+#pragma unroll
+  for (int k = 0; k < N; k++) { t2[k] = addc_co_0(s2[k], g[k], g[k]); e2[k] = subb_co_0(d2[k], b2[k], b2[k]); }
+#pragma unroll
+  for (int k = 0; k < N; k++) { t3[k] = addc_co_0(s3[k], g[k], g[k]); e3[k] = subb_0(d3[k], b2[k]); }
+#pragma unroll
+  for (int k = 0; k < N; k++) {
+    const uint64_t m = or_mask(c[k], g[k]);
+    sum[k] = join(sel(s0[k], t0[k], m), sel(s1[k], t1[k], m), sel(s2[k], t2[k], m), sel(s3[k], t3[k], m));
+    diff[k] = join(e0[k], e1[k], e2[k], e3[k]);
+  }
+}
 }  // namespace fpd

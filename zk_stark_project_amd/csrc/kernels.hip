@@ -401,14 +401,17 @@ __global__ __launch_bounds__(TPB) void k_eval_linear(EvalCommon c, LinearEvalArg
 constexpr uint32_t OOD_LOGE = 11;
 // Arrays a >= ntwo (the composition columns, whose OOD frame is at z only) skip
 // the second point (their partials at it are left zero).
+// A rank of a sharded proof evaluates the blocks [b0, b0 + gridDim.x) only;
+// partial[(a * gridDim.x + b - b0) * 2 + {0,1}] (the all-gathered rank blocks
+// are what k_eval_bitrev_tail reads).
 __global__ __launch_bounds__(TPB) void k_eval_bitrev(const felt* __restrict__ arrays, uint32_t logn, uint32_t logE,
                                                      const felt* __restrict__ pw0, const felt* __restrict__ pw1,
-                                                     uint32_t ntwo, felt* __restrict__ partial) {
+                                                     uint32_t ntwo, uint32_t b0, felt* __restrict__ partial) {
   __shared__ felt s0[TPB];
   __shared__ felt s1[TPB];
   const uint32_t E = 1u << logE;
   const bool two = blockIdx.y < ntwo;  // block-uniform
-  const felt* src = arrays + ((uint64_t)blockIdx.y << logn) + ((uint64_t)blockIdx.x << logE);
+  const felt* src = arrays + ((uint64_t)blockIdx.y << logn) + ((uint64_t)(b0 + blockIdx.x) << logE);
   const uint32_t t = threadIdx.x;
   // levels 0..2 in registers over the thread's 8 consecutive elements (E = 2048 = 8 * TPB),
   // the remaining levels over the TPB thread results in LDS
@@ -484,26 +487,32 @@ __global__ __launch_bounds__(TPB) void k_eval_bitrev(const felt* __restrict__ ar
 // second level of the OOD tree: the nb block partials of each (array, point)
 // (bit-reversed order continues: level logE + l uses pw[logn - 1 - logE - l]);
 // one block per array; nb <= 2 * 2048 (pairs are combined while loading).
+// The partials come in rank blocks of nbl = 2^lognbl blocks each (world 1: one
+// rank block): block b of array a at ((b / nbl * narrays + a) * nbl + b % nbl) * 2.
 __global__ __launch_bounds__(TPB) void k_eval_bitrev_tail(const felt* __restrict__ partial, uint32_t nb,
-                                                          uint32_t logn, uint32_t logE, const felt* __restrict__ pw0,
+                                                          uint32_t lognbl, uint32_t narrays, uint32_t logn,
+                                                          uint32_t logE, const felt* __restrict__ pw0,
                                                           const felt* __restrict__ pw1, felt ninv,
                                                           felt* __restrict__ out) {
   __shared__ felt s0[1u << OOD_LOGE];
   __shared__ felt s1[1u << OOD_LOGE];
-  const felt* src = partial + (uint64_t)blockIdx.x * nb * 2;
+  const uint32_t a = blockIdx.x, nblm = (1u << lognbl) - 1;
+  auto P = [&](uint32_t b, uint32_t k) {
+    return partial[((((uint64_t)(b >> lognbl) * narrays + a) << lognbl) + (b & nblm)) * 2 + k];
+  };
   uint32_t l = logE, m = nb;
   if (nb > (1u << OOD_LOGE)) {  // fold one level while loading
     const felt a0 = pw0[logn - 1 - l], a1 = pw1[logn - 1 - l];
     for (uint32_t i = threadIdx.x; i < nb / 2; i += TPB) {
-      s0[i] = add(src[4 * i], mul(a0, src[4 * i + 2]));
-      s1[i] = add(src[4 * i + 1], mul(a1, src[4 * i + 3]));
+      s0[i] = add(P(2 * i, 0), mul(a0, P(2 * i + 1, 0)));
+      s1[i] = add(P(2 * i, 1), mul(a1, P(2 * i + 1, 1)));
     }
     l++;
     m = nb / 2;
   } else {
     for (uint32_t i = threadIdx.x; i < nb; i += TPB) {
-      s0[i] = src[2 * i];
-      s1[i] = src[2 * i + 1];
+      s0[i] = P(i, 0);
+      s1[i] = P(i, 1);
     }
   }
   __syncthreads();
@@ -573,12 +582,14 @@ __global__ __launch_bounds__(TPB) void k_deep(DeepArgs a, const felt* __restrict
 // (bit-reversed, n-scaled like its inputs). LIN_CH positions per thread, TPB
 // apart; column-outer so each column's loads are in flight together. Its coset
 // LDE then replaces w column reads per LDE point of the pointwise k_deep by one.
+// A rank of a sharded proof combines the positions [p0, p0 + np) (out[0, np)).
 __global__ __launch_bounds__(TPB) void k_deep_lincomb(const felt* __restrict__ coef, uint32_t w, uint64_t n,
-                                                      const felt* __restrict__ gamma, felt* __restrict__ out) {
+                                                      uint64_t p0, uint64_t np, const felt* __restrict__ gamma,
+                                                      felt* __restrict__ out) {
   felt acc[LIN_CH];
   uint64_t p[LIN_CH];
   static_for<0, LIN_CH>([&](auto k) {
-    p[k] = LIN_POINT(k) < n ? LIN_POINT(k) : 0;
+    p[k] = p0 + (LIN_POINT(k) < np ? LIN_POINT(k) : 0);
     acc[k] = zero();
   });
   for (uint32_t c = 0; c < w; c++) {
@@ -589,7 +600,7 @@ __global__ __launch_bounds__(TPB) void k_deep_lincomb(const felt* __restrict__ c
     static_for<0, LIN_CH>([&](auto k) { acc[k] = add(acc[k], mul(g, v[k])); });
   }
   static_for<0, LIN_CH>([&](auto k) {
-    if (LIN_POINT(k) < n) out[LIN_POINT(k)] = acc[k];
+    if (LIN_POINT(k) < np) out[LIN_POINT(k)] = acc[k];
   });
 }
 
@@ -804,16 +815,30 @@ void launch_eval_linear(Prof& prof, hipStream_t s, const EvalCommon& c, const Li
            hipLaunchKernelGGL((k_eval_linear<true, true>), g, dim3(TPB), 0, s, c, a, lde, a.dinv, comp));
 }
 
+void launch_eval_bitrev_blocks(Prof& prof, hipStream_t s, const felt* arrays, uint32_t narrays, uint32_t ntwo,
+                               uint32_t logn, const felt* pw0, const felt* pw1, uint32_t b0, uint32_t nbl,
+                               felt* partial) {
+  const uint32_t logE = logn < OOD_LOGE ? logn : OOD_LOGE;
+  LAUNCH(prof, "eval_bitrev", s, (double)narrays * nbl * (1ull << logE) * 16.0,
+         hipLaunchKernelGGL(k_eval_bitrev, dim3(nbl, narrays), dim3(TPB), 0, s, arrays, logn, logE, pw0, pw1,
+                            ntwo, b0, partial));
+}
+
+void launch_eval_bitrev_tail(Prof& prof, hipStream_t s, const felt* partial, uint32_t narrays, uint32_t logn,
+                             uint32_t nbl, const felt* pw0, const felt* pw1, felt ninv, felt* out) {
+  const uint32_t logE = logn < OOD_LOGE ? logn : OOD_LOGE;
+  const uint32_t nb = 1u << (logn - logE);
+  LAUNCH(prof, "eval_bitrev_tail", s, (double)narrays * nb * 32.0,
+         hipLaunchKernelGGL(k_eval_bitrev_tail, dim3(narrays), dim3(TPB), 0, s, partial, nb,
+                            (uint32_t)kc::ilog2_u64(nbl), narrays, logn, logE, pw0, pw1, ninv, out));
+}
+
 void launch_eval_bitrev(Prof& prof, hipStream_t s, const felt* arrays, uint32_t narrays, uint32_t ntwo, uint32_t logn,
                         const felt* pw0, const felt* pw1, felt* partial, felt ninv, felt* out) {
-  uint32_t logE = logn < OOD_LOGE ? logn : OOD_LOGE;
-  uint32_t nb = 1u << (logn - logE);
-  LAUNCH(prof, "eval_bitrev", s, (double)narrays * (1ull << logn) * 16.0,
-         hipLaunchKernelGGL(k_eval_bitrev, dim3(nb, narrays), dim3(TPB), 0, s, arrays, logn, logE, pw0, pw1,
-                            ntwo, partial));
-  LAUNCH(prof, "eval_bitrev_tail", s, (double)narrays * nb * 32.0,
-         hipLaunchKernelGGL(k_eval_bitrev_tail, dim3(narrays), dim3(TPB), 0, s, partial, nb, logn, logE, pw0, pw1,
-                            ninv, out));
+  const uint32_t logE = logn < OOD_LOGE ? logn : OOD_LOGE;
+  const uint32_t nb = 1u << (logn - logE);
+  launch_eval_bitrev_blocks(prof, s, arrays, narrays, ntwo, logn, pw0, pw1, 0, nb, partial);
+  launch_eval_bitrev_tail(prof, s, partial, narrays, logn, nb, pw0, pw1, ninv, out);
 }
 
 void launch_deep_denominators(Prof& prof, hipStream_t s, const PointMap& m, uint64_t count, const felt* zz,
@@ -822,11 +847,11 @@ void launch_deep_denominators(Prof& prof, hipStream_t s, const PointMap& m, uint
   launch_den_inverse(prof, s, m, count, zero(), zero(), 1, binv, zz, pw);
 }
 
-void launch_deep_lincomb(Prof& prof, hipStream_t s, const felt* coef, uint32_t w, uint64_t n, const felt* gamma,
-                         felt* out) {
-  LAUNCH(prof, "deep_lincomb", s, (double)(w + 1) * n * 16.0,
-         hipLaunchKernelGGL(k_deep_lincomb, dim3(blocks_for((n + LIN_CH - 1) / LIN_CH)), dim3(TPB), 0, s, coef, w, n,
-                            gamma, out));
+void launch_deep_lincomb(Prof& prof, hipStream_t s, const felt* coef, uint32_t w, uint64_t n, uint64_t p0,
+                         uint64_t np, const felt* gamma, felt* out) {
+  LAUNCH(prof, "deep_lincomb", s, (double)(w + 1) * np * 16.0,
+         hipLaunchKernelGGL(k_deep_lincomb, dim3(blocks_for((np + LIN_CH - 1) / LIN_CH)), dim3(TPB), 0, s, coef, w, n,
+                            p0, np, gamma, out));
 }
 
 void launch_deep(Prof& prof, hipStream_t s, const DeepArgs& a, felt* out) {

@@ -383,16 +383,22 @@ __global__ __launch_bounds__(256) void k_merkle_lane(MerkleArgs a) {
 
 // ---- sharded commitments: the rank hashes the rows it owns (cosets
 // [j0, j0+Bl), rows t < rows) and scatters the digests by destination rank
-// (contiguous natural leaf ranges) for the all-to-all:
-// send[((s*Bl + jl)*rr + tl)], s = t / rr, tl = t % rr, rr = rows / R.
+// (contiguous natural leaf ranges) for the all-to-all. The exchange runs in
+// K = 2^logK chunks along the destination's rows (so chunk k's all-to-all
+// overlaps the hashing of chunk k+1): chunk k holds, for every destination s,
+// the rows t = s*rr + k*rc + tc (tc < rc = rr / K) at
+// send_k[((s*Bl + jl)*rc + tc)], rr = rows / R.
 template <int MODE>
 __global__ __launch_bounds__(TPB) void k_leaf_hash_shard(const felt* __restrict__ src, uint64_t n, uint32_t cols,
                                                          uint32_t logBl, uint32_t logrows, uint32_t logrr,
-                                                         uint32_t* __restrict__ send) {
+                                                         uint32_t logK, uint32_t k, uint32_t* __restrict__ send) {
   const uint64_t q = blockIdx.x * (uint64_t)TPB + threadIdx.x;
+  const uint32_t logrc = logrr - logK, logrk = logrows - logK;  // rows per chunk: per destination, in all
+  if (q >= (1ull << (logrk + logBl))) return;
+  const uint64_t jl = q >> logrk, u = q & ((1ull << logrk) - 1);
+  const uint64_t sd = u >> logrc, tc = u & ((1ull << logrc) - 1);
+  const uint64_t t = (sd << logrr) + ((uint64_t)k << logrc) + tc;
   const uint64_t rows = 1ull << logrows;
-  if (q >= (rows << logBl)) return;
-  const uint64_t jl = q >> logrows, t = q & (rows - 1);
   uint32_t d[8];
   if (MODE == 0) {  // LDE row t of coset jl: (c*Bl + jl)*n + t
     const felt* base = src + jl * n + t;
@@ -400,19 +406,21 @@ __global__ __launch_bounds__(TPB) void k_leaf_hash_shard(const felt* __restrict_
     b3::hash_felts([&](uint32_t c) { return base[c * cstride]; }, cols, d);
   } else {  // FRI row: positions t + k*rows of coset jl (16*rows per coset)
     const felt* base = src + (jl << (logrows + 4)) + t;
-    b3::hash_felts([&](uint32_t k) { return base[k * rows]; }, cols, d);
+    b3::hash_felts([&](uint32_t kk) { return base[kk * rows]; }, cols, d);
   }
-  const uint64_t s = t >> logrr, tl = t & ((1ull << logrr) - 1);
-  store_digest(send + ((((s << logBl) + jl) << logrr) + tl) * 8, d);
+  store_digest(send + ((((sd << logBl) + jl) << logrc) + tc) * 8, d);
 }
 
-// received leaf digests (source-rank-major = global coset j major, B cosets
-// of rr rows) -> natural leaf order of this rank's range: leaf j + B*tl
+// received leaf digests -> natural leaf order of this rank's range: chunk k
+// (L/K digests, source-rank-major = global coset j major, rc rows each) holds
+// the range rows tl = k*rc + tc: leaf j + B*tl
 __global__ __launch_bounds__(TPB) void k_leaf_unpack(const uint32_t* __restrict__ recv, uint32_t logB, uint32_t logrr,
-                                                     uint32_t* __restrict__ nodes, uint64_t L) {
+                                                     uint32_t logK, uint32_t* __restrict__ nodes, uint64_t L) {
   const uint64_t idx = blockIdx.x * (uint64_t)TPB + threadIdx.x;
   if (idx >= L) return;
-  const uint64_t j = idx >> logrr, tl = idx & ((1ull << logrr) - 1);
+  const uint32_t logrc = logrr - logK;
+  const uint64_t k = idx >> (logB + logrc), r = idx & ((1ull << (logB + logrc)) - 1);
+  const uint64_t j = r >> logrc, tl = (k << logrc) + (r & ((1ull << logrc) - 1));
   uint32_t d[8];
   load_digest(recv + idx * 8, d);
   store_digest(nodes + (L + j + (tl << logB)) * 8, d);
@@ -1233,23 +1241,24 @@ void launch_fri_tail(Prof& prof, hipStream_t s, const FriTailArgs& a) {
 }
 
 void launch_leaf_hash_shard(Prof& prof, hipStream_t s, int mode, const felt* src, uint64_t n, uint32_t cols,
-                            uint32_t logBl, uint32_t logrows, uint32_t logrr, uint32_t* send) {
-  const uint64_t cnt = 1ull << (logrows + logBl);
+                            uint32_t logBl, uint32_t logrows, uint32_t logrr, uint32_t logK, uint32_t k,
+                            uint32_t* send) {
+  const uint64_t cnt = 1ull << (logrows - logK + logBl);
   if (mode == 0)
     LAUNCH(prof, "leaf_hash_shard", s, (double)cnt * (cols * 16.0 + 32.0),
            hipLaunchKernelGGL(k_leaf_hash_shard<0>, dim3(blocks_for(cnt)), dim3(TPB), 0, s, src, n, cols, logBl,
-                              logrows, logrr, send));
+                              logrows, logrr, logK, k, send));
   else
     LAUNCH(prof, "leaf_hash_shard", s, (double)cnt * (cols * 16.0 + 32.0),
            hipLaunchKernelGGL(k_leaf_hash_shard<1>, dim3(blocks_for(cnt)), dim3(TPB), 0, s, src, n, cols, logBl,
-                              logrows, logrr, send));
+                              logrows, logrr, logK, k, send));
 }
 
 void launch_merkle_from_shards(Prof& prof, hipStream_t s, const uint32_t* recv, uint32_t logB, uint32_t logrr,
-                               uint32_t* nodes) {
+                               uint32_t logK, uint32_t* nodes) {
   const uint64_t L = 1ull << (logB + logrr);
   LAUNCH(prof, "leaf_unpack", s, (double)L * 64.0,
-         hipLaunchKernelGGL(k_leaf_unpack, dim3(blocks_for(L)), dim3(TPB), 0, s, recv, logB, logrr, nodes, L));
+         hipLaunchKernelGGL(k_leaf_unpack, dim3(blocks_for(L)), dim3(TPB), 0, s, recv, logB, logrr, logK, nodes, L));
   merkle_upper(prof, s, nodes, L, nullptr);
 }
 

@@ -272,11 +272,12 @@ struct zkp_ctx {
   }
   uint64_t next_session = 0;
   std::vector<hipEvent_t> up_ev;  // pipeline events (column-group uploads, per-column all-gathers)
-  void events(size_t k) {
-    if (up_ev.size() >= k) return;
-    for (hipEvent_t e : up_ev) HIP_CHECK(hipEventDestroy(e));
-    up_ev.assign(k, nullptr);
-    for (auto& e : up_ev) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  void events(size_t k) {  // grows only: events already recorded may still be waited on
+    while (up_ev.size() < k) {
+      hipEvent_t e;
+      HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      up_ev.push_back(e);
+    }
   }
 
   zkp_comm* self = nullptr;
@@ -363,10 +364,24 @@ bool commit_rows(zkp_ctx* ctx, zkp_comm* cm, int mode, const felt* src, uint64_t
   tr.Lr = 1ull << (logB + logrr);
   uint32_t* send = ctx->buf<uint32_t>("shard_send", (size_t)8 << (logBl + logrows));
   uint32_t* recv = ctx->buf<uint32_t>("shard_recv", (size_t)8 << (logBl + logrows));
-  launch_leaf_hash_shard(pf, st, mode, src, n, cols, logBl, logrows, logrr, send);
-  cm->all_to_all(st, send, recv, (size_t)32 << (logBl + logrr));
+  // the leaf-digest all-to-all in K chunks on the side stream, chunk k's exchange
+  // overlapping the hashing of chunk k+1 (every hash launch is queued before the
+  // first collective, so host-synchronous transports overlap too)
+  const uint32_t logK = logrr >= 12 ? 2u : 0u, K = 1u << logK;
+  const size_t chunk_words = (size_t)8 << (logBl + logrows - logK), block = (size_t)32 << (logBl + logrr - logK);
+  ctx->events(K + 1);
+  for (uint32_t k = 0; k < K; k++) {
+    launch_leaf_hash_shard(pf, st, mode, src, n, cols, logBl, logrows, logrr, logK, k, send + k * chunk_words);
+    HIP_CHECK(hipEventRecord(ctx->up_ev[k], st));
+  }
+  for (uint32_t k = 0; k < K; k++) {
+    HIP_CHECK(hipStreamWaitEvent(ctx->side, ctx->up_ev[k], 0));
+    cm->all_to_all(ctx->side, send + k * chunk_words, recv + k * chunk_words, block);
+  }
+  HIP_CHECK(hipEventRecord(ctx->up_ev[K], ctx->side));
+  HIP_CHECK(hipStreamWaitEvent(st, ctx->up_ev[K], 0));
   tr.nodes = ctx->buf<uint32_t>(name, (size_t)16 * tr.Lr);
-  launch_merkle_from_shards(pf, st, recv, logB, logrr, tr.nodes);
+  launch_merkle_from_shards(pf, st, recv, logB, logrr, logK, tr.nodes);
   uint32_t* roots = ctx->buf<uint32_t>("shard_roots", (size_t)8 * R);
   cm->all_gather(st, tr.nodes + 8, roots, 32);
   std::vector<uint8_t> hr((size_t)32 * R);
@@ -423,14 +438,29 @@ void fetch_all(zkp_ctx* ctx, const std::vector<Fetch>& fs) {
 // dpw[0..logn) / dpw[logn..2logn) are in device memory; returns the device
 // array ood[2a + {0,1}] (array a at the two points; arrays a >= ntwo at the
 // first point only, their second entry is zero)
+// Sharded (cm world R > 1, at least R blocks of 2048 coefficients): each rank
+// evaluates 1/R of every array's blocks (the partial Horner sums of SURVEY
+// §8(e)(4)), the rank blocks are all-gathered (narrays * nb * 32 bytes in all)
+// and every rank combines them: the same values as one rank evaluating it all.
 felt* ood_launch(zkp_ctx* ctx, const felt* arrays, uint32_t narrays, uint32_t ntwo, uint32_t logn,
-                 const felt* dpw) {
+                 const felt* dpw, zkp_comm* cm = nullptr) {
   uint32_t logE = logn < 11 ? logn : 11;
   if (logn - logE > 12) throw ZkpFail{ZKP_ERR_TRACE_SHAPE, "OOD evaluation supports n <= 2^23"};
-  felt* part = ctx->buf<felt>("ood_part", (size_t)2 * narrays * (1ull << (logn - logE)));
+  const uint32_t nb = 1u << (logn - logE);
+  felt* part = ctx->buf<felt>("ood_part", (size_t)2 * narrays * nb);
   felt* dv = ctx->buf<felt>("ood_vals", (size_t)2 * narrays);
-  launch_eval_bitrev(ctx->prof, ctx->stream, arrays, narrays, ntwo, logn, dpw, dpw + logn, part,
-                     inv(felt_u64(1ull << logn)), dv);
+  const felt ninv = inv(felt_u64(1ull << logn));
+  const uint32_t R = cm ? (uint32_t)cm->world : 1u;
+  if (R == 1 || nb < R) {
+    launch_eval_bitrev(ctx->prof, ctx->stream, arrays, narrays, ntwo, logn, dpw, dpw + logn, part, ninv, dv);
+    return dv;
+  }
+  const uint32_t nbl = nb / R;
+  felt* mine = ctx->buf<felt>("ood_part_rank", (size_t)2 * narrays * nbl);
+  launch_eval_bitrev_blocks(ctx->prof, ctx->stream, arrays, narrays, ntwo, logn, dpw, dpw + logn,
+                            (uint32_t)cm->rank * nbl, nbl, mine);
+  cm->all_gather(ctx->stream, mine, part, (size_t)2 * narrays * nbl * 16);
+  launch_eval_bitrev_tail(ctx->prof, ctx->stream, part, narrays, logn, nbl, dpw, dpw + logn, ninv, dv);
   return dv;
 }
 
@@ -565,16 +595,26 @@ std::vector<felt> comp_dft_consts(uint64_t n, uint32_t logce, uint32_t C) {
 // column and the composition columns with coefficients [1 | delta]: w column reads
 // per LDE point become one (C3: 8.2 GB -> ~1 GB per proof). Same field values.
 constexpr uint32_t DEEP_COEF_MIN_W = 16;
-void deep_evaluations(zkp_ctx* ctx, hipStream_t st, DeepArgs da, const felt* coef, uint64_t n, const felt* Sj0,
-                      uint32_t logN, felt* out) {
+// Sharded, each rank combines 1/R of the positions and the combined column is
+// all-gathered (n * 16 bytes in all) instead of every rank reading all w columns.
+void deep_evaluations(zkp_ctx* ctx, zkp_comm* cm, hipStream_t st, DeepArgs da, const felt* coef, uint64_t n,
+                      const felt* Sj0, uint32_t logN, felt* out) {
   static const bool pointwise_only = getenv("ZKP_DEEP_POINTWISE") != nullptr;  // A/B switch
   if (da.w < DEEP_COEF_MIN_W || pointwise_only) {
     launch_deep(ctx->prof, st, da, out);
     return;
   }
   const uint32_t Bl = 1u << da.logBl;
+  const uint32_t R = (uint32_t)cm->world;
   felt* acomb = ctx->buf<felt>("deep_acoef", n);
-  launch_deep_lincomb(ctx->prof, st, coef, da.w, n, da.gamma, acomb);
+  if (R == 1) {
+    launch_deep_lincomb(ctx->prof, st, coef, da.w, n, 0, n, da.gamma, acomb);
+  } else {
+    const uint64_t nR = n / R;
+    felt* mine = ctx->buf<felt>("deep_acoef_rank", nR);
+    launch_deep_lincomb(ctx->prof, st, coef, da.w, n, (uint64_t)cm->rank * nR, nR, da.gamma, mine);
+    cm->all_gather(st, mine, acomb, nR * 16);
+  }
   felt* alde = ctx->buf<felt>("deep_alde", (size_t)Bl * n);
   NttBatch lb{acomb, alde, Sj0, n, n, Bl, Bl, Bl};
   launch_ntt(ctx->prof, st, lb, da.logn, true, ctx->tws(logN), logN);
@@ -979,6 +1019,26 @@ int prove_impl(zkp_ctx* ctx, zkp_comm* cm, int air_id, const felt* d_trace, uint
   TreeShard ttree;
   bool coeffs_drawn = false;
   {
+    if (h_trace && R > 1) {
+      // sharded host trace: each rank uploads only its 1/R row
+      // slice of every column over PCIe; the slices are all-gathered over the
+      // comm (xGMI) into the whole trace on every rank, which then interpolates it
+      const uint64_t nR = n >> logR;
+      felt* dfull = const_cast<felt*>(d_trace);
+      felt* slice = ctx->buf<felt>("trace_slice", (size_t)w * nR);
+      HIP_CHECK(hipMemcpy2DAsync(slice, nR * 16, h_trace + (size_t)rank * nR, n * 16, nR * 16, w,
+                                 hipMemcpyHostToDevice, st));
+      if (w == 1) {
+        cm->all_gather(st, slice, dfull, nR * 16);
+      } else {  // rank blocks [s][col][nR] -> column-major [col][s*nR + t]
+        felt* gat = ctx->buf<felt>("trace_gather", (size_t)w * n);
+        cm->all_gather(st, slice, gat, (size_t)w * nR * 16);
+        for (uint32_t sr = 0; sr < R; sr++)
+          HIP_CHECK(hipMemcpy2DAsync(dfull + (size_t)sr * nR, n * 16, gat + (size_t)sr * w * nR, nR * 16, nR * 16, w,
+                                     hipMemcpyDeviceToDevice, st));
+      }
+      h_trace = nullptr;  // resident on every rank from here
+    }
     // column groups: one for device-resident traces; host traces upload group g+1
     // on the copy stream while the main stream interpolates and extends group g
     const uint32_t groups = h_trace ? (w >= 16 ? 8u : (w >= 4 ? 4u : 1u)) : 1u;
@@ -1108,7 +1168,7 @@ int prove_impl(zkp_ctx* ctx, zkp_comm* cm, int air_id, const felt* d_trace, uint
   if (!z_drawn) launch_dt_draw_z(pf, st, dt_seed, croot_d, wn_root, logn, dt_zz, dt_pw);
   ctx->stage_end("2_constraints_commit");
 
-  // 5. OOD frame (every rank holds all trace and composition coefficients)
+  // 5. OOD frame (sharded: every rank holds all coefficients and sums 1/R of each array's blocks)
   // the DEEP denominators (x - z)(x - zg) only need z: their batch-inversion
   // phases run on the side stream beside the OOD evaluation and its transcript
   felt* deep_binv = ctx->buf<felt>("binv", ((uint64_t)Bl * n) / 2048 + 1);
@@ -1119,7 +1179,7 @@ int prove_impl(zkp_ctx* ctx, zkp_comm* cm, int air_id, const felt* d_trace, uint
   HIP_CHECK(hipEventRecord(ctx->ev_join, ctx->side));
   // OOD frame and DEEP coefficients on the device (device transcript); the host
   // replays both at the FRI round trip
-  felt* dv = ood_launch(ctx, coef, w + C, w, logn, dt_pw);  // composition columns at z only
+  felt* dv = ood_launch(ctx, coef, w + C, w, logn, dt_pw, cm);  // composition columns at z only
   felt* dgam = ctx->buf<felt>("gamma", w + C);
   felt* dk = ctx->buf<felt>("dt_dk", 4);
   HIP_CHECK(hipMemcpyAsync(dk, dt_zz, 32, hipMemcpyDeviceToDevice, st));
@@ -1136,7 +1196,7 @@ int prove_impl(zkp_ctx* ctx, zkp_comm* cm, int air_id, const felt* d_trace, uint
     da.pm = deep_pm;
     da.binv = deep_binv;
     HIP_CHECK(hipStreamWaitEvent(st, ctx->ev_join, 0));
-    deep_evaluations(ctx, st, da, coef, n, Sj0, logN, deep);
+    deep_evaluations(ctx, cm, st, da, coef, n, Sj0, logN, deep);
   }
   ctx->stage_end("4_deep_launch");
 
@@ -2104,7 +2164,7 @@ int zkp_deep_fri(zkp_session* s, const zkp_felt* deep_coeffs, zkp_fri_channel ch
     da.tlde = s->get("tlde"); da.clde = s->get("clde"); da.gamma = dgam; da.dk = dk; da.g = g;
     da.pm = pm;
     da.binv = binv;
-    deep_evaluations(ctx, st, da, s->get("coef"), n, ctx->S(s->logn, s->logB), s->logN, deep);
+    deep_evaluations(ctx, ctx->self_comm(), st, da, s->get("coef"), n, ctx->S(s->logn, s->logB), s->logN, deep);
     // FriProver::build_layers: commit each layer, the caller's channel returns alpha, fold
     s->layers.assign(s->L + 1, FriLayer{});
     uint64_t tot = 0, D = s->N;

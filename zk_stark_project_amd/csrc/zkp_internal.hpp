@@ -96,10 +96,12 @@ bool merkle_upper(Prof& prof, hipStream_t s, uint32_t* nodes, uint64_t L, const 
 // sharded commitments: hash the shard's rows (mode 0: LDE rows of cols columns;
 // mode 1: FRI rows of 16) into per-destination blocks; then, after the
 // all-to-all, rebuild the natural-order leaves of this rank's range and its subtree
+// all-to-all in 2^logK chunks along the destination rows: launch_leaf_hash_shard hashes chunk k
 void launch_leaf_hash_shard(Prof& prof, hipStream_t s, int mode, const felt* src, uint64_t n, uint32_t cols,
-                            uint32_t logBl, uint32_t logrows, uint32_t logrr, uint32_t* send);
+                            uint32_t logBl, uint32_t logrows, uint32_t logrr, uint32_t logK, uint32_t k,
+                            uint32_t* send);
 void launch_merkle_from_shards(Prof& prof, hipStream_t s, const uint32_t* recv, uint32_t logB, uint32_t logrr,
-                               uint32_t* nodes);
+                               uint32_t logK, uint32_t* nodes);
 // internal nodes nodes[1..L) from leaves nodes[L..2L)
 void launch_merkle_tree(Prof& prof, hipStream_t s, uint32_t* nodes, uint64_t L);
 constexpr uint32_t PACK_MAX = 16;
@@ -226,6 +228,14 @@ void launch_comp_dft(Prof& prof, hipStream_t s, const felt* recv, const uint32_t
 // (arrays a >= ntwo at x0 only)
 void launch_eval_bitrev(Prof& prof, hipStream_t s, const felt* arrays, uint32_t narrays, uint32_t ntwo, uint32_t logn,
                         const felt* pw0, const felt* pw1, felt* partial, felt ninv, felt* out);
+// its two halves for a sharded proof: a rank evaluates the 2048-coefficient blocks
+// [b0, b0 + nbl) of every array (partial[(a * nbl + b - b0) * 2 + k]); after the
+// all-gather of those rank blocks the tail combines all n / 2048 of them
+void launch_eval_bitrev_blocks(Prof& prof, hipStream_t s, const felt* arrays, uint32_t narrays, uint32_t ntwo,
+                               uint32_t logn, const felt* pw0, const felt* pw1, uint32_t b0, uint32_t nbl,
+                               felt* partial);
+void launch_eval_bitrev_tail(Prof& prof, hipStream_t s, const felt* partial, uint32_t narrays, uint32_t logn,
+                             uint32_t nbl, const felt* pw0, const felt* pw1, felt ninv, felt* out);
 
 // DEEP composition over the LDE domain (natural order out)
 struct DeepArgs {
@@ -247,8 +257,8 @@ void launch_deep(Prof& prof, hipStream_t s, const DeepArgs& a, felt* out);
 // coefficient-form DEEP for wide traces (winterfell combines the trace polynomials
 // before extending): out[p] = sum_{c < w} gamma[c] * coef[c*n + p]
 // over the bit-reversed, n-scaled coefficient columns -> one combined column (same layout)
-void launch_deep_lincomb(Prof& prof, hipStream_t s, const felt* coef, uint32_t w, uint64_t n, const felt* gamma,
-                         felt* out);
+void launch_deep_lincomb(Prof& prof, hipStream_t s, const felt* coef, uint32_t w, uint64_t n, uint64_t p0,
+                         uint64_t np, const felt* gamma, felt* out);  // positions [p0, p0 + np) -> out[0, np)
 
 // FRI fold-by-F (F = 16) over coset-major evaluations of the cosets [j0, j0+Bl)
 // (16*m16 positions each): natural row r = j + B*t', x_r = off * w_D^r; alpha read from device

@@ -176,19 +176,21 @@ class GlobalUpdateProver(Prover):
         out[:, len(rows):] = packed[:, -1:]
         return TraceTable(out)
 
-    def build_trace_device(self, ctx=None):
+    def build_trace_device(self, ctx=None, d_out=None):
         """build_trace() on the GPU (zkp_build_global_update_trace): returns the device
         pointer of the 120 x n column-major trace in HBM (caller frees it with
-        ctx.free) and keeps the final state for get_pub_inputs()."""
+        ctx.free; d_out = an existing allocation of 120 * n * 16 bytes to reuse) and
+        keeps the final state for get_pub_inputs()."""
         ctx = ctx or self.context()
         raw = _flatten(self.raw_global_w, self.raw_global_b)
         local = [_flatten(w, b) for w, b in zip(self.local_w, self.local_b)]
         n = self.trace_length
-        d = ctx.alloc(2 * D_STATE * n * 16)
+        d = d_out if d_out is not None else ctx.alloc(2 * D_STATE * n * 16)
         try:
             self._final_state = ctx.build_global_update_trace(raw, self.blinding, local, self.k, n, d)
         except Exception:
-            ctx.free(d)
+            if d_out is None:
+                ctx.free(d)
             raise
         return d
 

@@ -25,8 +25,9 @@ import threading
 from . import _native
 
 
-def prove_local_group(world: int, air_id: int, trace, pub, options, contexts=None, devices=None):
-    """Run one sharded proof with `world` in-process ranks; returns [(bytes, transcript)] per rank."""
+def prove_local_group(world: int, air_id: int, trace, pub, options, contexts=None, devices=None, shape=None):
+    """Run one sharded proof with `world` in-process ranks; returns [(bytes, transcript)] per rank.
+    `trace` is a host array, or (shape=(width, n)) a device pointer every rank can read."""
     comms = _native.local_group(world)
     if contexts is None:
         devices = devices or [0] * world
@@ -36,7 +37,7 @@ def prove_local_group(world: int, air_id: int, trace, pub, options, contexts=Non
 
     def run(r):
         try:
-            results[r] = contexts[r].prove_sharded(comms[r], air_id, trace, pub, options)
+            results[r] = contexts[r].prove_sharded(comms[r], air_id, trace, pub, options, shape=shape)
         except Exception as e:  # noqa: BLE001 — re-raised below
             errors[r] = e
 
