@@ -8,4 +8,5 @@ timeout -k 10 720 python -u -m pytest tests -m gpu -x -q -v --timeout 120 --time
 grep -E "passed|failed|PASSED.*c5|slowest" gpurun_out/t1.log | tail -5
 timeout -k 10 240 python bench.py --steps 20 --stats > gpurun_out/b1.json 2> gpurun_out/b1.err || { tail -20 gpurun_out/b1.err; exit 1; }
 timeout -k 10 200 python bench.py --air agg --steps 10 --no-cpu-baseline --stats > gpurun_out/b1agg.json 2> gpurun_out/b1agg.err || { tail -20 gpurun_out/b1agg.err; exit 1; }
+timeout -k 10 120 python3 scripts/timeline.py > gpurun_out/timeline.txt 2>&1 || { tail -5 gpurun_out/timeline.txt; exit 1; }
 echo ALLOK

@@ -60,47 +60,92 @@ ZKP_HD void compress(uint32_t cv[8], const uint32_t m[16], uint64_t counter, uin
   cv[4] = s4 ^ s12; cv[5] = s5 ^ s13; cv[6] = s6 ^ s14; cv[7] = s7 ^ s15;
 }
 
+// The same compression with its 7 rounds as a loop (the message permuted in
+// registers between rounds, BLAKE3's MSG_PERMUTATION): ~7x less code than
+// compress(). For latency-bound code that runs on few waves per CU (tree tops,
+// the device transcript, the FRI tail), whose fully unrolled straight-line
+// code otherwise streams through a cold instruction cache.
+ZKP_HD void compress_r(uint32_t cv[8], const uint32_t m_in[16], uint64_t counter, uint32_t block_len,
+                       uint32_t flags) {
+  uint32_t m[16];
+  for (int i = 0; i < 16; i++) m[i] = m_in[i];
+  uint32_t s0 = cv[0], s1 = cv[1], s2 = cv[2], s3 = cv[3], s4 = cv[4], s5 = cv[5], s6 = cv[6], s7 = cv[7];
+  uint32_t s8 = 0x6A09E667u, s9 = 0xBB67AE85u, s10 = 0x3C6EF372u, s11 = 0xA54FF53Au;
+  uint32_t s12 = (uint32_t)counter, s13 = (uint32_t)(counter >> 32), s14 = block_len, s15 = flags;
+#pragma unroll 1
+  for (int r = 0; r < 7; r++) {
+    B3_ROUND(0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15)
+    const uint32_t t0 = m[2], t1 = m[6], t2 = m[3], t3 = m[10], t4 = m[7], t5 = m[0], t6 = m[4], t7 = m[13];
+    const uint32_t t8 = m[1], t9 = m[11], t10 = m[12], t11 = m[5], t12 = m[9], t13 = m[14], t14 = m[15],
+                   t15 = m[8];
+    m[0] = t0; m[1] = t1; m[2] = t2; m[3] = t3; m[4] = t4; m[5] = t5; m[6] = t6; m[7] = t7;
+    m[8] = t8; m[9] = t9; m[10] = t10; m[11] = t11; m[12] = t12; m[13] = t13; m[14] = t14; m[15] = t15;
+  }
+  cv[0] = s0 ^ s8; cv[1] = s1 ^ s9; cv[2] = s2 ^ s10; cv[3] = s3 ^ s11;
+  cv[4] = s4 ^ s12; cv[5] = s5 ^ s13; cv[6] = s6 ^ s14; cv[7] = s7 ^ s15;
+}
+
 ZKP_HD void set_iv(uint32_t cv[8]) {
   for (int i = 0; i < 8; i++) cv[i] = iv(i);
 }
 
+// compress() or its rolled form (ROLLED: latency-bound call sites, see compress_r)
+template <bool ROLLED>
+ZKP_HD void compress_t(uint32_t cv[8], const uint32_t m[16], uint64_t counter, uint32_t block_len, uint32_t flags) {
+  if constexpr (ROLLED)
+    compress_r(cv, m, counter, block_len, flags);
+  else
+    compress(cv, m, counter, block_len, flags);
+}
+
 // merge(a, b) = BLAKE3(a || b): one 64-byte block, single chunk, root
+template <bool ROLLED = false>
 ZKP_HD void merge(const uint32_t a[8], const uint32_t b[8], uint32_t out[8]) {
   uint32_t m[16];
   for (int i = 0; i < 8; i++) { m[i] = a[i]; m[8 + i] = b[i]; }
   set_iv(out);
-  compress(out, m, 0, 64, CHUNK_START | CHUNK_END | ROOT);
+  compress_t<ROLLED>(out, m, 0, 64, CHUNK_START | CHUNK_END | ROOT);
 }
 
 // parent node of the BLAKE3 chunk tree
+template <bool ROLLED = false>
 ZKP_HD void parent(const uint32_t l[8], const uint32_t r[8], bool root, uint32_t out[8]) {
   uint32_t m[16];
   for (int i = 0; i < 8; i++) { m[i] = l[i]; m[8 + i] = r[i]; }
   set_iv(out);
-  compress(out, m, 0, 64, PARENT | (root ? ROOT : 0u));
+  compress_t<ROLLED>(out, m, 0, 64, PARENT | (root ? ROOT : 0u));
 }
 
 // chaining value of chunk `ci` covering felts [f0, f1) (at most 64 felts = 1024 bytes)
-template <typename Get>
+// The next block's felts are fetched before the current block is compressed
+// (a register double buffer), so a row read from HBM overlaps its hashing
+// instead of waiting once per 64-byte block.
+template <bool ROLLED = false, typename Get>
 ZKP_HD void hash_chunk(Get get, uint32_t f0, uint32_t f1, uint64_t ci, bool root, uint32_t cv[8]) {
   set_iv(cv);
   uint32_t nblocks = f1 > f0 ? (f1 - f0 + 3) / 4 : 1;
+  felt cur[4];
+#pragma unroll
+  for (int k = 0; k < 4; k++) cur[k] = f0 + k < f1 ? get(f0 + k) : fp::zero();
   for (uint32_t b = 0; b < nblocks; b++) {
+    const uint32_t base = f0 + 4 * b, nb = base + 4;
+    felt nxt[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) nxt[k] = b + 1 < nblocks && nb + k < f1 ? get(nb + k) : fp::zero();
     uint32_t m[16];
-    uint32_t base = f0 + 4 * b;
-    uint32_t cnt = 0;
 #pragma unroll
     for (int k = 0; k < 4; k++) {
-      felt v = fp::zero();
-      if (base + k < f1) { v = get(base + k); cnt++; }
-      m[4 * k + 0] = (uint32_t)v.lo;
-      m[4 * k + 1] = (uint32_t)(v.lo >> 32);
-      m[4 * k + 2] = (uint32_t)v.hi;
-      m[4 * k + 3] = (uint32_t)(v.hi >> 32);
+      m[4 * k + 0] = (uint32_t)cur[k].lo;
+      m[4 * k + 1] = (uint32_t)(cur[k].lo >> 32);
+      m[4 * k + 2] = (uint32_t)cur[k].hi;
+      m[4 * k + 3] = (uint32_t)(cur[k].hi >> 32);
     }
+    const uint32_t cnt = f1 - base < 4 ? f1 - base : 4;  // (nblocks = 1 with f1 == f0: cnt = 0)
     uint32_t fl = (b == 0 ? CHUNK_START : 0u) | (b == nblocks - 1 ? CHUNK_END : 0u);
     if (root && b == nblocks - 1) fl |= ROOT;
-    compress(cv, m, ci, 16 * cnt, fl);
+    compress_t<ROLLED>(cv, m, ci, 16 * (f1 > f0 ? cnt : 0u), fl);
+#pragma unroll
+    for (int k = 0; k < 4; k++) cur[k] = nxt[k];
   }
 }
 
@@ -131,6 +176,29 @@ ZKP_HD void hash_felts(Get get, uint32_t nf, uint32_t out[8]) {
   uint32_t r[8];
   parent(c2, c3, false, r);
   parent(l, r, true, out);
+}
+
+// hash_elements over a compile-time count NF <= 64 felts (one chunk): the block
+// loop is unrolled, so get(k) sees constant k (register-resident rows, no scratch)
+template <int NF, int B = 0, typename Get>
+ZKP_HD void hash_felts_c(Get get, uint32_t cv[8]) {
+  static_assert(NF >= 1 && NF <= 64, "one chunk");
+  constexpr int NB = (NF + 3) / 4;
+  if constexpr (B == 0) set_iv(cv);
+  uint32_t m[16];
+  constexpr int cnt = NF - 4 * B < 4 ? NF - 4 * B : 4;
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    felt v = fp::zero();
+    if (k < cnt) v = get(4 * B + k);
+    m[4 * k + 0] = (uint32_t)v.lo;
+    m[4 * k + 1] = (uint32_t)(v.lo >> 32);
+    m[4 * k + 2] = (uint32_t)v.hi;
+    m[4 * k + 3] = (uint32_t)(v.hi >> 32);
+  }
+  constexpr uint32_t fl = (B == 0 ? CHUNK_START : 0u) | (B == NB - 1 ? (CHUNK_END | ROOT) : 0u);
+  compress(cv, m, 0, 16 * cnt, fl);
+  if constexpr (B + 1 < NB) hash_felts_c<NF, B + 1>(get, cv);
 }
 
 // ---------------------------------------------------------------- host one-shot

@@ -4,6 +4,8 @@
 // the FRI layers (fold-by-16, the fused small-layer tail, the remainder).
 #include "kernels_dev.hpp"
 
+#include <cstdlib>
+
 using kc::rev_bits;
 using kc::static_for;
 
@@ -151,10 +153,55 @@ __device__ __forceinline__ void compress_quad(const uint32_t m[16], uint32_t q, 
   b ^= d;
 }
 
+// compress_quad with its rounds as a loop: the 16 message words are permuted in
+// registers between rounds (BLAKE3 MSG_PERMUTATION), so each round selects the
+// same word slots. ~6x less code, for the narrow tree levels that run on few
+// waves per CU (their fully unrolled code streams through a cold I-cache).
+__device__ __forceinline__ void compress_quad_r(const uint32_t m_in[16], uint32_t q, uint32_t flags, uint32_t& a,
+                                                uint32_t& b) {
+  uint32_t m[16];
+#pragma unroll
+  for (int i = 0; i < 16; i++) m[i] = m_in[i];
+  uint32_t c = sel4(q, b3::iv(0), b3::iv(1), b3::iv(2), b3::iv(3));
+  uint32_t d = sel4(q, 0u, 0u, 64u, flags);
+#define B3Q_G(x, y)                 \
+  a = a + b + (x);                  \
+  d = b3::rotr(d ^ a, 16);          \
+  c = c + d;                        \
+  b = b3::rotr(b ^ c, 12);          \
+  a = a + b + (y);                  \
+  d = b3::rotr(d ^ a, 8);           \
+  c = c + d;                        \
+  b = b3::rotr(b ^ c, 7);
+#pragma unroll 1
+  for (int r = 0; r < 7; r++) {
+    B3Q_G(sel4(q, m[0], m[2], m[4], m[6]), sel4(q, m[1], m[3], m[5], m[7]))
+    b = quad_rot<1>(b);
+    c = quad_rot<2>(c);
+    d = quad_rot<3>(d);
+    B3Q_G(sel4(q, m[8], m[10], m[12], m[14]), sel4(q, m[9], m[11], m[13], m[15]))
+    b = quad_rot<3>(b);
+    c = quad_rot<2>(c);
+    d = quad_rot<1>(d);
+    const uint32_t t0 = m[2], t1 = m[6], t2 = m[3], t3 = m[10], t4 = m[7], t5 = m[0], t6 = m[4], t7 = m[13];
+    const uint32_t t8 = m[1], t9 = m[11], t10 = m[12], t11 = m[5], t12 = m[9], t13 = m[14], t14 = m[15],
+                   t15 = m[8];
+    m[0] = t0; m[1] = t1; m[2] = t2; m[3] = t3; m[4] = t4; m[5] = t5; m[6] = t6; m[7] = t7;
+    m[8] = t8; m[9] = t9; m[10] = t10; m[11] = t11; m[12] = t12; m[13] = t13; m[14] = t14; m[15] = t15;
+  }
+#undef B3Q_G
+  a ^= c;
+  b ^= d;
+}
+
+template <bool ROLLED = false>
 __device__ __forceinline__ void merge_quad(const uint32_t m[16], uint32_t q, uint32_t& o0, uint32_t& o1) {
   o0 = sel4(q, b3::iv(0), b3::iv(1), b3::iv(2), b3::iv(3));
   o1 = sel4(q, b3::iv(4), b3::iv(5), b3::iv(6), b3::iv(7));
-  compress_quad(m, q, b3::CHUNK_START | b3::CHUNK_END | b3::ROOT, o0, o1);
+  if constexpr (ROLLED)
+    compress_quad_r(m, q, b3::CHUNK_START | b3::CHUNK_END | b3::ROOT, o0, o1);
+  else
+    compress_quad(m, q, b3::CHUNK_START | b3::CHUNK_END | b3::ROOT, o0, o1);
 }
 
 // Quad-cooperative digest of one FRI row of 16 felts (256 bytes: one chunk of
@@ -176,16 +223,17 @@ __device__ __forceinline__ void fri_leaf_quad(const MerkleArgs& a, uint64_t i, u
       m[4 * k + 3] = (uint32_t)(v.hi >> 32);
     }
     const uint32_t fl = (blk == 0 ? b3::CHUNK_START : 0u) | (blk == 3 ? (b3::CHUNK_END | b3::ROOT) : 0u);
-    compress_quad(m, q, fl, o0, o1);
+    compress_quad_r(m, q, fl, o0, o1);
   }
 }
 
+template <bool ROLLED = false>
 __device__ __forceinline__ void merge8(const uint32_t l[8], const uint32_t r[8], uint32_t out[8]) {
   uint32_t m[16];
 #pragma unroll
   for (int i = 0; i < 8; i++) { m[i] = l[i]; m[8 + i] = r[i]; }
   b3::set_iv(out);
-  b3::compress(out, m, 0, 64, b3::CHUNK_START | b3::CHUNK_END | b3::ROOT);
+  b3::compress_t<ROLLED>(out, m, 0, 64, b3::CHUNK_START | b3::CHUNK_END | b3::ROOT);
 }
 
 __device__ __forceinline__ void merkle_tail_op(const MerkleTail& tl, const uint32_t* root);
@@ -228,7 +276,7 @@ __global__ __launch_bounds__(256) void k_merkle_fused(MerkleArgs a) {
         store_digest(a.nodes + (L + base + 2 * t) * 8, d0);
         store_digest(a.nodes + (L + base + 2 * t + 1) * 8, d1);
       }
-      merge8(d0, d1, m);
+      merge8<true>(d0, d1, m);
       store_digest(a.nodes + ((L >> 1) + (base >> 1) + t) * 8, m);
 #pragma unroll
       for (int i = 0; i < 8; i++) sd[t * 9 + i] = m[i];
@@ -246,7 +294,7 @@ __global__ __launch_bounds__(256) void k_merkle_fused(MerkleArgs a) {
         uint32_t mm[16];
 #pragma unroll
         for (int i = 0; i < 8; i++) { mm[i] = sd[(2 * nd) * 9 + i]; mm[8 + i] = sd[(2 * nd + 1) * 9 + i]; }
-        merge_quad(mm, q, o0, o1);
+        merge_quad<true>(mm, q, o0, o1);
       }
       lvl >>= 1;
       lbase >>= 1;
@@ -265,7 +313,7 @@ __global__ __launch_bounds__(256) void k_merkle_fused(MerkleArgs a) {
       uint32_t l[8], r[8];
 #pragma unroll
       for (int i = 0; i < 8; i++) { l[i] = sd[(2 * t) * 9 + i]; r[i] = sd[(2 * t + 1) * 9 + i]; }
-      merge8(l, r, o);
+      merge8<true>(l, r, o);
     }
     lvl >>= 1;
     lbase >>= 1;
@@ -296,7 +344,7 @@ __global__ __launch_bounds__(256) void k_merkle_fused(MerkleArgs a) {
         const uint32_t* src = a.nodes + (uint64_t)(G + 2 * nd) * 8;  // the node's two children, adjacent
 #pragma unroll
         for (int k = 0; k < 16; k++) mm[k] = src[k];
-        merge_quad(mm, q, o0, o1);
+        merge_quad<true>(mm, q, o0, o1);
         sd[nd * 9 + q] = o0;
         sd[nd * 9 + 4 + q] = o1;
         uint32_t* dst = a.nodes + (uint64_t)(G / 2 + nd) * 8;
@@ -308,7 +356,7 @@ __global__ __launch_bounds__(256) void k_merkle_fused(MerkleArgs a) {
         uint32_t l[8], r[8], o[8];
         load_digest(a.nodes + (uint64_t)(G + 2 * i) * 8, l);
         load_digest(a.nodes + (uint64_t)(G + 2 * i + 1) * 8, r);
-        merge8(l, r, o);
+        merge8<true>(l, r, o);
         store_digest(a.nodes + (uint64_t)(G / 2 + i) * 8, o);
 #pragma unroll
         for (int k = 0; k < 8; k++) sd[i * 9 + k] = o[k];
@@ -323,7 +371,7 @@ __global__ __launch_bounds__(256) void k_merkle_fused(MerkleArgs a) {
           uint32_t mm[16];
 #pragma unroll
           for (int k = 0; k < 8; k++) { mm[k] = sd[(2 * nd) * 9 + k]; mm[8 + k] = sd[(2 * nd + 1) * 9 + k]; }
-          merge_quad(mm, q, o0, o1);
+          merge_quad<true>(mm, q, o0, o1);
         }
         __syncthreads();
         if (t < 4 * sl) {
@@ -340,7 +388,7 @@ __global__ __launch_bounds__(256) void k_merkle_fused(MerkleArgs a) {
         uint32_t l[8], r[8];
 #pragma unroll
         for (int k = 0; k < 8; k++) { l[k] = sd[(2 * t) * 9 + k]; r[k] = sd[(2 * t + 1) * 9 + k]; }
-        merge8(l, r, o);
+        merge8<true>(l, r, o);
       }
       __syncthreads();
       if (t < sl) {
@@ -373,6 +421,34 @@ __device__ __forceinline__ void lane_subtree(const MerkleArgs& a, uint64_t base,
   }
 }
 
+// Leaf pass of an LDE-row tree for narrow rows (COLS <= 8 felts): each lane
+// loads BOTH of its rows' felts before any hashing, then hashes them and
+// merges (as k_merkle_lane<0, 1>). The generic lane kernel reads each row
+// inside its hash and its digest stores may alias the LDE (no restrict), so
+// the second row's loads wait behind the first row's hash and stores; here the
+// HBM latency of both rows is exposed once per lane.
+template <int COLS>
+__global__ __launch_bounds__(256) void k_merkle_leaf2(MerkleArgs a) {
+  const uint64_t lane = blockIdx.x * (uint64_t)256 + threadIdx.x;
+  if (lane >= (a.L >> 1)) return;
+  const uint64_t cstride = a.n << a.logB, bmask = (1ull << a.logB) - 1;
+  felt v[2][COLS];
+#pragma unroll
+  for (int r = 0; r < 2; r++) {
+    const uint64_t i = 2 * lane + r;
+    const felt* base = a.src + (i & bmask) * a.n + (i >> a.logB);
+#pragma unroll
+    for (int c = 0; c < COLS; c++) v[r][c] = base[c * cstride];
+  }
+  uint32_t d0[8], d1[8], m[8];
+  b3::hash_felts_c<COLS>([&](int c) { return v[0][c]; }, d0);
+  b3::hash_felts_c<COLS>([&](int c) { return v[1][c]; }, d1);
+  store_digest(a.nodes + (a.L + 2 * lane) * 8, d0);
+  store_digest(a.nodes + (a.L + 2 * lane + 1) * 8, d1);
+  merge8(d0, d1, m);
+  store_digest(a.nodes + ((a.L >> 1) + lane) * 8, m);
+}
+
 template <int MODE, int H>
 __global__ __launch_bounds__(256) void k_merkle_lane(MerkleArgs a) {
   const uint64_t lane = blockIdx.x * (uint64_t)256 + threadIdx.x;
@@ -388,7 +464,9 @@ __global__ __launch_bounds__(256) void k_merkle_lane(MerkleArgs a) {
 // overlaps the hashing of chunk k+1): chunk k holds, for every destination s,
 // the rows t = s*rr + k*rc + tc (tc < rc = rr / K) at
 // send_k[((s*Bl + jl)*rc + tc)], rr = rows / R.
-template <int MODE>
+// COLS > 0 (narrow LDE rows, MODE 0): the row's felts are loaded into registers
+// before hashing (compile-time row length, see k_merkle_leaf2)
+template <int MODE, int COLS = 0>
 __global__ __launch_bounds__(TPB) void k_leaf_hash_shard(const felt* __restrict__ src, uint64_t n, uint32_t cols,
                                                          uint32_t logBl, uint32_t logrows, uint32_t logrr,
                                                          uint32_t logK, uint32_t k, uint32_t* __restrict__ send) {
@@ -400,7 +478,14 @@ __global__ __launch_bounds__(TPB) void k_leaf_hash_shard(const felt* __restrict_
   const uint64_t t = (sd << logrr) + ((uint64_t)k << logrc) + tc;
   const uint64_t rows = 1ull << logrows;
   uint32_t d[8];
-  if (MODE == 0) {  // LDE row t of coset jl: (c*Bl + jl)*n + t
+  if constexpr (MODE == 0 && COLS > 0) {
+    const felt* base = src + jl * n + t;
+    const uint64_t cstride = n << logBl;
+    felt v[COLS];
+#pragma unroll
+    for (int c = 0; c < COLS; c++) v[c] = base[c * cstride];
+    b3::hash_felts_c<COLS>([&](int c) { return v[c]; }, d);
+  } else if (MODE == 0) {  // LDE row t of coset jl: (c*Bl + jl)*n + t
     const felt* base = src + jl * n + t;
     const uint64_t cstride = n << logBl;
     b3::hash_felts([&](uint32_t c) { return base[c * cstride]; }, cols, d);
@@ -439,7 +524,7 @@ __device__ __forceinline__ void dcoin_reseed(uint32_t s[8], const uint32_t d[8])
   uint32_t m[16];
   for (int i = 0; i < 8; i++) { m[i] = s[i]; m[8 + i] = d[i]; }
   b3::set_iv(s);
-  b3::compress(s, m, 0, 64, b3::CHUNK_START | b3::CHUNK_END | b3::ROOT);
+  b3::compress_r(s, m, 0, 64, b3::CHUNK_START | b3::CHUNK_END | b3::ROOT);
 }
 __device__ __forceinline__ felt dcoin_candidate(const uint32_t s[8], uint64_t ctr) {
   uint32_t m[16], o[8];
@@ -448,7 +533,7 @@ __device__ __forceinline__ felt dcoin_candidate(const uint32_t s[8], uint64_t ct
   m[9] = (uint32_t)(ctr >> 32);
   for (int i = 10; i < 16; i++) m[i] = 0;
   b3::set_iv(o);
-  b3::compress(o, m, 0, 40, b3::CHUNK_START | b3::CHUNK_END | b3::ROOT);
+  b3::compress_r(o, m, 0, 40, b3::CHUNK_START | b3::CHUNK_END | b3::ROOT);
   return fp::make((uint64_t)o[0] | ((uint64_t)o[1] << 32), (uint64_t)o[2] | ((uint64_t)o[3] << 32));
 }
 // sequential draw (thread-local), advancing *ctr
@@ -502,7 +587,7 @@ __device__ __forceinline__ void hash_felts_block(Get get, uint32_t nf, uint32_t 
   for (uint32_t c = threadIdx.x; c < nch; c += blockDim.x) {
     uint32_t cv[8];
     const uint32_t f0 = 64 * c, f1 = f0 + 64 < nf ? f0 + 64 : nf;
-    b3::hash_chunk(get, f0, f1, c, nch == 1, cv);
+    b3::hash_chunk<true>(get, f0, f1, c, nch == 1, cv);
     for (int i = 0; i < 8; i++) s_cv[c][i] = cv[i];
   }
   __syncthreads();
@@ -523,7 +608,7 @@ __device__ __forceinline__ void hash_felts_block(Get get, uint32_t nf, uint32_t 
           uint32_t l[8], p[8];
           --top;
           for (int i = 0; i < 8; i++) l[i] = st[top][i];
-          b3::parent(l, cv, false, p);
+          b3::parent<true>(l, cv, false, p);
           for (int i = 0; i < 8; i++) cv[i] = p[i];
           total >>= 1;
         }
@@ -536,7 +621,7 @@ __device__ __forceinline__ void hash_felts_block(Get get, uint32_t nf, uint32_t 
         uint32_t l[8], p[8];
         top--;
         for (int i = 0; i < 8; i++) l[i] = st[top][i];
-        b3::parent(l, cv, top == 0, p);
+        b3::parent<true>(l, cv, top == 0, p);
         for (int i = 0; i < 8; i++) cv[i] = p[i];
       }
       for (int i = 0; i < 8; i++) out[i] = cv[i];
@@ -682,7 +767,7 @@ __device__ __forceinline__ void coin_fri_step(uint32_t* __restrict__ seed, const
   uint32_t m[16], s[8];
   for (int i = 0; i < 8; i++) { m[i] = seed[i]; m[8 + i] = root[i]; root_out[i] = root[i]; }
   b3::set_iv(s);
-  b3::compress(s, m, 0, 64, b3::CHUNK_START | b3::CHUNK_END | b3::ROOT);
+  b3::compress_r(s, m, 0, 64, b3::CHUNK_START | b3::CHUNK_END | b3::ROOT);
   felt a = fp::zero();
   for (uint32_t ctr = 1; ctr <= 1000; ctr++) {
     for (int i = 0; i < 8; i++) m[i] = s[i];
@@ -691,7 +776,7 @@ __device__ __forceinline__ void coin_fri_step(uint32_t* __restrict__ seed, const
     for (int i = 10; i < 16; i++) m[i] = 0;
     uint32_t o[8];
     b3::set_iv(o);
-    b3::compress(o, m, 0, 40, b3::CHUNK_START | b3::CHUNK_END | b3::ROOT);
+    b3::compress_r(o, m, 0, 40, b3::CHUNK_START | b3::CHUNK_END | b3::ROOT);
     felt v = fp::make((uint64_t)o[0] | ((uint64_t)o[1] << 32), (uint64_t)o[2] | ((uint64_t)o[3] << 32));
     if (!fp::ge_p(v)) { a = v; break; }
   }
@@ -721,6 +806,34 @@ __global__ __launch_bounds__(TPB) void k_pack(PackArgs a, uint32_t* __restrict__
     dst[o + i] = src[i];
 }
 
+// FriProver::set_remainder's interpolation by a whole block: the D = m*B last-layer
+// values (coset-major: natural index i = j + B*t at E[j*m + t]) -> the first ncoef
+// coefficients c_k = D^-1 off^-k sum_i v_i w_D^-ik into s_c. The powers w_D^-j are
+// a table (one pow per thread); each wave sums the D terms of one coefficient
+// (lanes over i, then a shuffle reduction), so the chain is ~log D products long
+// instead of 2D sequential ones. D <= 256 (host-checked); s_tw holds D felts.
+__device__ __forceinline__ felt shfl_down_felt(felt v, int d) {
+  const int a = __shfl_down((int)(uint32_t)v.lo, d), b = __shfl_down((int)(uint32_t)(v.lo >> 32), d);
+  const int c = __shfl_down((int)(uint32_t)v.hi, d), e = __shfl_down((int)(uint32_t)(v.hi >> 32), d);
+  return fp::make((uint64_t)(uint32_t)a | ((uint64_t)(uint32_t)b << 32),
+                  (uint64_t)(uint32_t)c | ((uint64_t)(uint32_t)e << 32));
+}
+__device__ __forceinline__ void remainder_coeffs_block(const felt* __restrict__ E, uint32_t logB, uint32_t m,
+                                                       uint32_t ncoef, felt off_inv, felt wd_inv, felt d_inv,
+                                                       felt* s_c, felt* s_tw) {
+  const uint32_t D = m << logB, t = threadIdx.x, lane = t & 63, wave = t >> 6, nw = blockDim.x >> 6;
+  for (uint32_t j = t; j < D; j += blockDim.x) s_tw[j] = fp::pow_u64(wd_inv, j);
+  __syncthreads();
+  for (uint32_t k = wave; k < ncoef; k += nw) {
+    felt acc = zero();
+    for (uint32_t i = lane; i < D; i += 64)
+      acc = add(acc, mul(E[(i & ((1u << logB) - 1)) * m + (i >> logB)], s_tw[(i * k) & (D - 1)]));
+    for (int d = 32; d >= 1; d >>= 1) acc = add(acc, shfl_down_felt(acc, d));
+    if (lane == 0) s_c[k] = mul(mul(acc, d_inv), fp::pow_u64(off_inv, k));
+  }
+  __syncthreads();
+}
+
 // FriProver::set_remainder on the device for small last layers (D <= 256): the
 // D values E (coset-major: natural index i = j + B*t at E[j*m + t]) interpolated
 // over off*<w_D>, the first ncoef = D/B coefficients kept:
@@ -732,20 +845,10 @@ __global__ __launch_bounds__(TPB) void k_fri_remainder(const felt* __restrict__ 
                                                        uint32_t* __restrict__ seed, felt* __restrict__ rem_out,
                                                        uint32_t* __restrict__ commit_out) {
   __shared__ felt s_c[256];
+  __shared__ felt s_tw[256];
   __shared__ uint32_t s_cv[32][8];
-  const uint32_t D = m << logB;
-  for (uint32_t k = threadIdx.x; k < ncoef; k += TPB) {
-    const felt wk = fp::pow_u64(wd_inv, k);
-    felt p = one(), acc = zero();
-    for (uint32_t i = 0; i < D; i++) {
-      acc = add(acc, mul(E[(i & ((1u << logB) - 1)) * m + (i >> logB)], p));
-      p = mul(p, wk);
-    }
-    const felt c = mul(mul(acc, d_inv), fp::pow_u64(off_inv, k));
-    s_c[k] = c;
-    rem_out[k] = c;
-  }
-  __syncthreads();
+  remainder_coeffs_block(E, logB, m, ncoef, off_inv, wd_inv, d_inv, s_c, s_tw);
+  for (uint32_t k = threadIdx.x; k < ncoef; k += TPB) rem_out[k] = s_c[k];
   uint32_t h[8];
   hash_felts_block([&](uint32_t i) { return s_c[i]; }, ncoef, h, s_cv);
   if (threadIdx.x == 0) {
@@ -830,7 +933,7 @@ __global__ void k_query_positions(const uint32_t* __restrict__ seedp, const unsi
 #pragma unroll
   for (int k = 10; k < 16; k++) m[k] = 0;
   b3::set_iv(s2);
-  b3::compress(s2, m, 0, 40, b3::CHUNK_START | b3::CHUNK_END | b3::ROOT);
+  b3::compress_r(s2, m, 0, 40, b3::CHUNK_START | b3::CHUNK_END | b3::ROOT);
   for (uint32_t i = threadIdx.x; i < q; i += blockDim.x) {
 #pragma unroll
     for (int k = 0; k < 8; k++) m[k] = s2[k];
@@ -840,7 +943,7 @@ __global__ void k_query_positions(const uint32_t* __restrict__ seedp, const unsi
     for (int k = 10; k < 16; k++) m[k] = 0;
     uint32_t out[8];
     b3::set_iv(out);
-    b3::compress(out, m, 0, 40, b3::CHUNK_START | b3::CHUNK_END | b3::ROOT);
+    b3::compress_r(out, m, 0, 40, b3::CHUNK_START | b3::CHUNK_END | b3::ROOT);
     pos[i] = ((uint64_t)out[0] | ((uint64_t)out[1] << 32)) & (N - 1);
   }
 }
@@ -972,6 +1075,7 @@ __global__ __launch_bounds__(TPB) void k_fri_fold16(const felt* __restrict__ E, 
 __global__ __launch_bounds__(512) void k_fri_tail(FriTailArgs a) {
   __shared__ uint32_t sd[128 * 9];
   __shared__ felt s_c[256];
+  __shared__ felt s_tw[256];
   __shared__ uint32_t s_cv[32][8];
   const uint32_t t = threadIdx.x, nd = t >> 2, q = t & 3;
   for (uint32_t l = 0; l < a.nl; l++) {
@@ -998,7 +1102,7 @@ __global__ __launch_bounds__(512) void k_fri_tail(FriTailArgs a) {
         uint32_t mm[16];
 #pragma unroll
         for (int i = 0; i < 8; i++) { mm[i] = sd[(2 * nd) * 9 + i]; mm[8 + i] = sd[(2 * nd + 1) * 9 + i]; }
-        merge_quad(mm, q, o0, o1);
+        merge_quad<true>(mm, q, o0, o1);
       }
       __syncthreads();
       if (nd < s) {
@@ -1024,20 +1128,9 @@ __global__ __launch_bounds__(512) void k_fri_tail(FriTailArgs a) {
   }
   // remainder: interpolate the last layer (D = m * B points) into ncoef = m
   // coefficients, commit, reseed (k_fri_remainder)
-  const uint32_t m = a.rem_m, D = m << a.logB;
-  const felt* E = a.rem_E;
-  for (uint32_t k = t; k < m; k += blockDim.x) {
-    const felt wk = fp::pow_u64(a.wd_inv, k);
-    felt p = one(), acc = zero();
-    for (uint32_t i = 0; i < D; i++) {
-      acc = add(acc, mul(E[(i & ((1u << a.logB) - 1)) * m + (i >> a.logB)], p));
-      p = mul(p, wk);
-    }
-    const felt c = mul(mul(acc, a.d_inv), fp::pow_u64(a.rem_off_inv, k));
-    s_c[k] = c;
-    a.rem_out[k] = c;
-  }
-  __syncthreads();
+  const uint32_t m = a.rem_m;
+  remainder_coeffs_block(a.rem_E, a.logB, m, m, a.rem_off_inv, a.wd_inv, a.d_inv, s_c, s_tw);
+  for (uint32_t k = t; k < m; k += blockDim.x) a.rem_out[k] = s_c[k];
   uint32_t h[8];
   hash_felts_block([&](uint32_t i) { return s_c[i]; }, m, h, s_cv);
   if (t == 0) {
@@ -1068,6 +1161,9 @@ static void merkle_pass(Prof& prof, hipStream_t s, const MerkleArgs& a, uint32_t
 // upper levels: wide levels by lane passes (4 levels each), the narrow top by
 // the LDS-fused kernel (9 levels per launch, parallel tail)
 bool merkle_upper(Prof& prof, hipStream_t s, uint32_t* nodes, uint64_t L, const MerkleTail* tail) {
+  // ZKP_MERKLE_LANE_MIN=k (A/B switch): lane passes down to 2^k nodes (default 18)
+  static const uint32_t lane_min_log =
+      getenv("ZKP_MERKLE_LANE_MIN") ? std::max(2, atoi(getenv("ZKP_MERKLE_LANE_MIN"))) : 18u;
   while (L > 1) {
     MerkleArgs a{};
     a.nodes = nodes;
@@ -1075,7 +1171,7 @@ bool merkle_upper(Prof& prof, hipStream_t s, uint32_t* nodes, uint64_t L, const 
     // lane passes only while they have >= 2^14 lanes (4 levels, 15 serial merges
     // per lane); below that the 9-level LDS-fused blocks have the shorter
     // critical path (9 merges) and fill more CUs
-    if (L >= (1ull << 18)) {
+    if (L >= (1ull << lane_min_log)) {
       // 2 levels per lane: measured faster than 3-4 (fewer live digests, more waves;
       // tests/native/kbench_merkle.cpp, profiles/r02_kbench_merkle.txt)
       merkle_pass<2>(prof, s, a, 2, "merkle_upper", (double)L * 32.0 * 1.5);
@@ -1105,7 +1201,18 @@ bool launch_merkle_lde(Prof& prof, hipStream_t s, const felt* lde, uint32_t cols
   // each lane hashes 2 rows and merges them (H = 1): measured faster than deeper
   // lane subtrees, whose extra live digests cost waves (kbench_merkle.cpp)
   const uint32_t H = L >= 2 ? 1 : 0;
-  merkle_pass<0>(prof, s, a, H, "merkle_lde", (double)L * (cols * 16.0 + 64.0));
+  static const bool no_preload = getenv("ZKP_NO_LEAF_PRELOAD") != nullptr;  // A/B switch
+  if (H == 1 && cols <= 8 && !no_preload) {
+    const double bytes = (double)L * (cols * 16.0 + 48.0);
+    const dim3 g(blocks_for(L >> 1));
+#define ZKP_LEAF2(CC) \
+  case CC: LAUNCH(prof, "merkle_lde", s, bytes, hipLaunchKernelGGL(k_merkle_leaf2<CC>, g, dim3(256), 0, s, a)); break;
+    switch (cols) { ZKP_LEAF2(1) ZKP_LEAF2(2) ZKP_LEAF2(3) ZKP_LEAF2(4) ZKP_LEAF2(5) ZKP_LEAF2(6) ZKP_LEAF2(7)
+                    ZKP_LEAF2(8) }
+#undef ZKP_LEAF2
+  } else {
+    merkle_pass<0>(prof, s, a, H, "merkle_lde", (double)L * (cols * 16.0 + 64.0));
+  }
   return merkle_upper(prof, s, nodes, L >> H, tail);
 }
 
@@ -1244,15 +1351,27 @@ void launch_leaf_hash_shard(Prof& prof, hipStream_t s, int mode, const felt* src
                             uint32_t logBl, uint32_t logrows, uint32_t logrr, uint32_t logK, uint32_t k,
                             uint32_t* send) {
   const uint64_t cnt = 1ull << (logrows - logK + logBl);
-  if (mode == 0)
-    LAUNCH(prof, "leaf_hash_shard", s, (double)cnt * (cols * 16.0 + 32.0),
-           hipLaunchKernelGGL(k_leaf_hash_shard<0>, dim3(blocks_for(cnt)), dim3(TPB), 0, s, src, n, cols, logBl,
+  const double bytes = (double)cnt * (cols * 16.0 + 32.0);
+  const dim3 g(blocks_for(cnt));
+#define ZKP_SHARD_LEAF(CC)                                                                                   \
+  case CC:                                                                                                   \
+    LAUNCH(prof, "leaf_hash_shard", s, bytes,                                                                \
+           hipLaunchKernelGGL((k_leaf_hash_shard<0, CC>), g, dim3(TPB), 0, s, src, n, cols, logBl, logrows, \
+                              logrr, logK, k, send));                                                        \
+    break;
+  if (mode == 0 && cols <= 8) {
+    switch (cols) { ZKP_SHARD_LEAF(1) ZKP_SHARD_LEAF(2) ZKP_SHARD_LEAF(3) ZKP_SHARD_LEAF(4) ZKP_SHARD_LEAF(5)
+                    ZKP_SHARD_LEAF(6) ZKP_SHARD_LEAF(7) ZKP_SHARD_LEAF(8) }
+  } else if (mode == 0)
+    LAUNCH(prof, "leaf_hash_shard", s, bytes,
+           hipLaunchKernelGGL(k_leaf_hash_shard<0>, g, dim3(TPB), 0, s, src, n, cols, logBl,
                               logrows, logrr, logK, k, send));
   else
     LAUNCH(prof, "leaf_hash_shard", s, (double)cnt * (cols * 16.0 + 32.0),
            hipLaunchKernelGGL(k_leaf_hash_shard<1>, dim3(blocks_for(cnt)), dim3(TPB), 0, s, src, n, cols, logBl,
                               logrows, logrr, logK, k, send));
 }
+#undef ZKP_SHARD_LEAF
 
 void launch_merkle_from_shards(Prof& prof, hipStream_t s, const uint32_t* recv, uint32_t logB, uint32_t logrr,
                                uint32_t logK, uint32_t* nodes) {
