@@ -306,6 +306,14 @@ def sharded_leg(ctx, rank: int, world: int, dist, local_rank: int, on_timeout=No
     pub = wl["prover"].get_pub_inputs(wl["trace"]).to_elements()
     comm = rccl_group_comm(ctx, rank, world)
     try:
+        # fabric check first (zkp_comm_check: verified RCCL all-to-all + all-gather of
+        # 64 MiB blocks) — the per-rank xGMI rates DESIGN.md §6's model assumes
+        blk = 64 << 20
+        a2a_ms, ag_ms = ctx.comm_check(comm, blk)
+        moved = (world - 1) * blk / 1e9
+        fabric = {"block_MiB": blk >> 20, "all_to_all_ms": round(a2a_ms, 3), "all_gather_ms": round(ag_ms, 3),
+                  "all_to_all_GBps_per_rank": round(moved / (a2a_ms / 1e3), 1),
+                  "all_gather_GBps_per_rank": round(moved / (ag_ms / 1e3), 1)}
         steps = 10
 
         def once():
@@ -318,7 +326,7 @@ def sharded_leg(ctx, rank: int, world: int, dist, local_rank: int, on_timeout=No
     return {"metric": "STARK proofs/sec + prove-time ms, MiMC AIR 2^22-step trace, one proof domain-sharded over "
                       "all GPUs", "workload": wl["workload"], "value": round(steps / elapsed, 3), "unit": "proofs/s",
             "ms_per_proof": round(elapsed / steps * 1e3, 3), "steps": steps, "warmup": 2, "scaling": "strong",
-            "parallelism": f"coset-sharded{world} (RCCL)", "proof_bytes": len(proof),
+            "parallelism": f"coset-sharded{world} (RCCL)", "proof_bytes": len(proof), "fabric": fabric,
             "bytes_per_proof_8d": sum(stage_bytes(1, 1 << 22, 8, 8, 6).values())}
 
 

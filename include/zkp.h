@@ -165,6 +165,13 @@ int zkp_comm_host_create(int world, int rank, const zkp_host_transport* transpor
 void zkp_comm_destroy(zkp_comm* comm);
 int zkp_comm_rank(const zkp_comm* comm);
 int zkp_comm_world(const zkp_comm* comm);
+/* Fabric check before proving (collective; no reference counterpart): one
+ * all-to-all of world blocks of block_bytes (multiple of 4) and one all-gather
+ * of block_bytes per rank, each run twice on the context's stream with
+ * rank-tagged words verified on the host. a2a_ms / ag_ms (nullable) receive
+ * the faster round's wall time of each collective on this rank. A mismatch
+ * is ZKP_ERR_DEVICE naming the peer and word. */
+int zkp_comm_check(zkp_ctx* ctx, zkp_comm* comm, uint64_t block_bytes, double* a2a_ms, double* ag_ms);
 /* Collective: every rank of `comm` must call it with the same arguments. */
 int zkp_prove_sharded(zkp_ctx* ctx, zkp_comm* comm, zkp_air_id air, const zkp_felt* trace_cols,
                       uint32_t width, uint64_t n, const zkp_felt* pub_elems, uint64_t n_pub,

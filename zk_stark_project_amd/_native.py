@@ -71,7 +71,8 @@ EXPORTED = [
     "zkp_copy_to_host", "zkp_trace_lde_commit", "zkp_merkle_commit_rows", "zkp_grind",
     "zkp_set_profiling", "zkp_kernel_stats", "zkp_reset_stats", "zkp_kernel_stats_table",
     "zkp_build_mimc_trace", "zkp_prove_sharded", "zkp_comm_local_group", "zkp_comm_rccl_unique_id",
-    "zkp_comm_rccl_create", "zkp_comm_destroy", "zkp_comm_rank", "zkp_comm_world", "zkp_prove_sharded_device",
+    "zkp_comm_rccl_create", "zkp_comm_destroy", "zkp_comm_rank", "zkp_comm_world", "zkp_comm_check",
+    "zkp_prove_sharded_device",
     "zkp_verify", "zkp_build_global_update_trace", "zkp_set_profiling_kernel",
     "zkp_session_create", "zkp_session_destroy", "zkp_session_trace_lde", "zkp_eval_constraints",
     "zkp_composition_commit", "zkp_ood_frame", "zkp_deep_fri", "zkp_query", "zkp_comm_host_create",
@@ -162,6 +163,8 @@ def load():
         L.zkp_comm_destroy.restype = None
         L.zkp_comm_rank.argtypes = [vp]
         L.zkp_comm_world.argtypes = [vp]
+        L.zkp_comm_check.argtypes = [vp, vp, ctypes.c_uint64, ctypes.POINTER(ctypes.c_double),
+                                     ctypes.POINTER(ctypes.c_double)]
         L.zkp_verify.argtypes = [i32, ctypes.c_char_p, u64, vp, u64, popt]
         L.zkp_verify.restype = i32
         L.zkp_build_global_update_trace.argtypes = [vp, vp, vp, vp, u64, Felt, u64, vp, vp]
@@ -355,6 +358,14 @@ class Context:
         data = ctypes.string_at(out, olen.value)
         self.lib.zkp_free(out)
         return data, tr
+
+    def comm_check(self, comm: "Comm", block_bytes: int = 1 << 20):
+        """zkp_comm_check (collective): verified all-to-all + all-gather of
+        `block_bytes` blocks; returns (all_to_all_ms, all_gather_ms) on this rank."""
+        ta, tg = ctypes.c_double(), ctypes.c_double()
+        self._check(self.lib.zkp_comm_check(self.ptr, comm.ptr, block_bytes, ctypes.byref(ta), ctypes.byref(tg)),
+                    "zkp_comm_check")
+        return ta.value, tg.value
 
     def rccl_comm(self, unique_id: bytes, world: int, rank: int) -> "Comm":
         p = ctypes.c_void_p()

@@ -1012,13 +1012,48 @@ int prove_impl(zkp_ctx* ctx, zkp_comm* cm, int air_id, const felt* d_trace, uint
   const felt* twn = ctx->tws(logN) + ((1ull << (logn - 1)) - 1);
   ctx->stage_end("0_setup");
 
-  // 2. trace LDE + commitment (DefaultTraceLde::new): interpolation on every
-  // rank, coset LDE of this rank's cosets, sharded row commitment
+  // 2. trace LDE + commitment (DefaultTraceLde::new): interpolation (by column
+  // over the ranks for wide traces), coset LDE of this rank's cosets, sharded
+  // row commitment
   felt* coef = ctx->buf<felt>("coef", (size_t)(w + C) * n);
   felt* tlde = ctx->buf<felt>("tlde", (size_t)w * Bl * n);
   TreeShard ttree;
   bool coeffs_drawn = false;
-  {
+  // wide traces shard the interpolation by column (cpt columns per rank) when the
+  // width divides over the ranks; narrow ones interpolate on every rank
+  const uint32_t cpt = (R > 1 && w % R == 0 && w >= 2 * R) ? w / R : 0;
+  if (cpt) {
+    // column-sharded interpolation: in round k rank r interpolates
+    // columns [k*R*cpr + r*cpr, +cpr) — uploading only those columns of a host
+    // trace — and round k's coefficient all-gather (side stream) lands its R*cpr
+    // columns in order at coef + k*R*cpr*n while the main stream extends round
+    // k - 1's columns on this rank's cosets. Nothing but coefficients crosses xGMI.
+    // rounds: the most that divide cpt, up to 6 — only round 0's exchange is
+    // exposed (C5 at R = 8: 5 rounds of 3 columns per rank, 24 columns per LDE)
+    uint32_t K = 6;
+    while (cpt % K) K--;
+    const uint32_t cpr = cpt / K;
+    felt* own = ctx->buf<felt>("coef_own", (size_t)cpt * n);
+    ctx->events(2 * (size_t)K);
+    for (uint32_t k = 0; k < K; k++) {
+      const uint64_t cown = (uint64_t)k * R * cpr + (uint64_t)rank * cpr;
+      felt* dcol = const_cast<felt*>(d_trace) + cown * n;
+      if (h_trace)
+        HIP_CHECK(hipMemcpyAsync(dcol, h_trace + cown * n, (size_t)cpr * n * 16, hipMemcpyHostToDevice, st));
+      NttBatch ib{dcol, own + (size_t)k * cpr * n, nullptr, n, n, 1, 1, cpr};
+      launch_ntt(pf, st, ib, logn, false, ctx->itws(logN), logN);
+      HIP_CHECK(hipEventRecord(ctx->up_ev[k], st));
+    }
+    for (uint32_t k = 0; k < K; k++) {
+      const uint64_t c0 = (uint64_t)k * R * cpr;
+      HIP_CHECK(hipStreamWaitEvent(ctx->side, ctx->up_ev[k], 0));
+      cm->all_gather(ctx->side, own + (size_t)k * cpr * n, coef + c0 * n, (size_t)cpr * n * 16);
+      HIP_CHECK(hipEventRecord(ctx->up_ev[K + k], ctx->side));
+      HIP_CHECK(hipStreamWaitEvent(st, ctx->up_ev[K + k], 0));
+      NttBatch lb{coef + c0 * n, tlde + c0 * Bl * n, Sj0, n, n, Bl, Bl, R * cpr * Bl};
+      launch_ntt(pf, st, lb, logn, true, ctx->tws(logN), logN);
+    }
+  } else {
     if (h_trace && R > 1) {
       // sharded host trace: each rank uploads only its 1/R row
       // slice of every column over PCIe; the slices are all-gathered over the
@@ -1064,6 +1099,8 @@ int prove_impl(zkp_ctx* ctx, zkp_comm* cm, int air_id, const felt* d_trace, uint
       NttBatch lb{coef + (size_t)c0 * n, tlde + (size_t)c0 * Bl * n, Sj0, n, n, Bl, Bl, cw * Bl};
       launch_ntt(pf, st, lb, logn, true, ctx->tws(logN), logN);
     }
+  }
+  {
     // unsharded: the tree's last block also reseeds with the root and draws the
     // composition coefficients (MERKLE_TAIL_DRAW_COEFFS)
     MerkleTail draw{};
@@ -1690,6 +1727,53 @@ int zkp_comm_host_create(int world, int rank, const zkp_host_transport* t, zkp_c
 }
 
 void zkp_comm_destroy(zkp_comm* comm) { delete comm; }
+
+int zkp_comm_check(zkp_ctx* ctx, zkp_comm* comm, uint64_t block_bytes, double* a2a_ms, double* ag_ms) {
+  int rc = guarded(ctx, [&] {
+    ctx->err.clear();
+    HIP_CHECK(hipSetDevice(ctx->device));
+    if (!comm || block_bytes == 0 || (block_bytes & 3)) return (int)ZKP_ERR_ARGUMENT;
+    const uint32_t W = (uint32_t)comm->world, me = (uint32_t)comm->rank;
+    const uint64_t words = block_bytes / 4;
+    // rank-tagged words: tag(src, dst, i); dst = W marks the all-gather block
+    auto tag = [](uint32_t src, uint32_t dst, uint64_t i) {
+      return ((src + 1) * 0x9E3779B1u) ^ ((dst + 7) * 0x85EBCA77u) ^ ((uint32_t)i * 0xC2B2AE3Du) ^ (uint32_t)(i >> 32);
+    };
+    std::vector<uint32_t> h((size_t)W * words);
+    for (uint32_t s = 0; s < W; s++)
+      for (uint64_t i = 0; i < words; i++) h[s * words + i] = tag(me, s, i);
+    uint32_t* send = ctx->buf<uint32_t>("cc_send", (size_t)W * words);
+    uint32_t* recv = ctx->buf<uint32_t>("cc_recv", (size_t)W * words);
+    ctx->upload(send, h.data(), h.size() * 4);
+    ctx->sync();
+    auto timed = [&](bool a2a) {
+      double best = 1e30;
+      for (int it = 0; it < 2; it++) {  // the first round also sets up the transport's connections
+        HIP_CHECK(hipMemsetAsync(recv, 0, (size_t)W * block_bytes, ctx->stream));
+        ctx->sync();
+        auto t0 = std::chrono::steady_clock::now();
+        if (a2a) comm->all_to_all(ctx->stream, send, recv, block_bytes);
+        else comm->all_gather(ctx->stream, send, recv, block_bytes);
+        ctx->sync();
+        best = std::min(best, std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+      }
+      ctx->download(h.data(), recv, h.size() * 4);
+      for (uint32_t s = 0; s < W; s++)
+        for (uint64_t i = 0; i < words; i++)
+          if (h[s * words + i] != (a2a ? tag(s, me, i) : tag(s, 0, i)))
+            throw ZkpFail{ZKP_ERR_DEVICE, std::string(a2a ? "all_to_all" : "all_gather") + ": block from rank " +
+                                              std::to_string(s) + " differs at word " + std::to_string(i)};
+      return best;
+    };
+    // the all-gather sends block 0 of `send`, i.e. tag(me, 0, i)
+    const double ta = timed(true), tg = timed(false);
+    if (a2a_ms) *a2a_ms = ta;
+    if (ag_ms) *ag_ms = tg;
+    return 0;
+  });
+  if (rc && comm) comm->abort();
+  return rc;
+}
 
 int zkp_comm_rank(const zkp_comm* comm) { return comm ? comm->rank : -1; }
 int zkp_comm_world(const zkp_comm* comm) { return comm ? comm->world : -1; }
