@@ -397,6 +397,82 @@ __global__ __launch_bounds__(TPB) void k_eval_linear(EvalCommon c, LinearEvalArg
   });
 }
 
+// Linear AIRs in coefficient form. Every term of their constraints is linear in
+// the trace, so the sums k_eval_linear forms per CE point are polynomials:
+//   A  = sum_c a_c T_c(w_n X) + b_c T_c(X)  (transition numerator; T_c(w_n X) has
+//        coefficients w_n^d t_{c,d}),  B0 = sum_c beta0_c T_c,  B1 = sum_c beta1_c T_c.
+// k_lin_lincomb forms their coefficients over the bit-reversed positions
+// [p0, p0 + np) of the coefficient columns (one read of each column, 3 products
+// per coefficient instead of 6 per CE point over ce cosets); the prover extends
+// them to its CE cosets and k_eval_linear_pts applies k_eval_linear's final
+// formula point by point: the same field values.
+// out = [A (TRANS) | B0 | B1 (TWO)], np felts each; twn[j] = w_n^j (j < n/2).
+template <bool TRANS, bool TWO>
+__global__ __launch_bounds__(TPB) void k_lin_lincomb(const felt* __restrict__ coef, uint32_t W, uint32_t logn,
+                                                     uint64_t p0, uint64_t np, const felt* __restrict__ coefs,
+                                                     const felt* __restrict__ twn, felt* __restrict__ out) {
+  const uint64_t n = 1ull << logn;
+  felt sa[LIN_CH], sb[LIN_CH], s0[LIN_CH], s1[LIN_CH];
+  uint64_t p[LIN_CH];
+  static_for<0, LIN_CH>([&](auto k) {
+    p[k] = p0 + (LIN_POINT(k) < np ? LIN_POINT(k) : 0);
+    sa[k] = zero(); sb[k] = zero(); s0[k] = zero(); s1[k] = zero();
+  });
+  for (uint32_t c = 0; c < W; c++) {
+    const felt* col = coef + (uint64_t)c * n;
+    felt v[LIN_CH];
+    static_for<0, LIN_CH>([&](auto k) { v[k] = col[p[k]]; });
+    if (TRANS) {
+      const felt ca = coefs[c], cb = coefs[W + c];
+      static_for<0, LIN_CH>([&](auto k) { sa[k] = add(sa[k], mul(ca, v[k])); sb[k] = add(sb[k], mul(cb, v[k])); });
+    }
+    const felt b0 = coefs[2 * W + c];
+    static_for<0, LIN_CH>([&](auto k) { s0[k] = add(s0[k], mul(b0, v[k])); });
+    if (TWO) {
+      const felt b1 = coefs[3 * W + c];
+      static_for<0, LIN_CH>([&](auto k) { s1[k] = add(s1[k], mul(b1, v[k])); });
+    }
+  }
+  static_for<0, LIN_CH>([&](auto k) {
+    const uint64_t i = LIN_POINT(k);
+    if (i >= np) return;
+    felt* o = out + i;
+    if (TRANS) {
+      const uint64_t d = __brevll(p[k]) >> (64 - logn);  // the coefficient's degree
+      const felt wd = d < (n >> 1) ? twn[d] : neg(twn[d - (n >> 1)]);
+      *o = add(mul(wd, sa[k]), sb[k]);
+      o += np;
+    }
+    *o = s0[k];
+    if (TWO) o[np] = s1[k];
+  });
+}
+
+// k_eval_linear's final formula over the extended arrays ev = [A | B0 | B1]
+// (each cel*n, CE-coset-major like comp)
+template <bool TRANS, bool TWO>
+__global__ __launch_bounds__(TPB) void k_eval_linear_pts(EvalCommon c, LinearEvalArgs a, const felt* __restrict__ ev,
+                                                         const felt* __restrict__ dinv, felt* __restrict__ comp) {
+  const uint64_t M = (uint64_t)c.cel << c.logn;
+  const felt* eb0 = TRANS ? ev + M : ev;
+  const felt bconst = a.coefs[4 * a.width], bconst1 = a.coefs[4 * a.width + 1];
+  static_for<0, LIN_CH>([&](auto k) {
+    const uint64_t q = LIN_POINT(k);
+    if (q >= M) return;
+    const uint32_t u = c.u0 + (uint32_t)(q >> c.logn);
+    felt x = point_x(c.pm, q);
+    felt tpart = TRANS ? mul(mul(ev[q], sub(x, c.w_last)), c.zinv[u]) : zero();
+    felt bnum;
+    if (TWO) {
+      felt e0 = sub(x, a.w_bstep), e1 = sub(x, a.w_bstep1);
+      bnum = add(mul(sub(eb0[q], bconst), e1), mul(sub(eb0[M + q], bconst1), e0));
+    } else {
+      bnum = sub(eb0[q], bconst);
+    }
+    comp[q] = add(tpart, mul(bnum, dinv[q]));
+  });
+}
+
 // bit-reversed polynomial evaluation: tree with level multipliers x^(2^l)
 constexpr uint32_t OOD_LOGE = 11;
 // Arrays a >= ntwo (the composition columns, whose OOD frame is at z only) skip
@@ -813,6 +889,37 @@ void launch_eval_linear(Prof& prof, hipStream_t s, const EvalCommon& c, const Li
   else
     LAUNCH(prof, "eval_linear", s, bytes,
            hipLaunchKernelGGL((k_eval_linear<true, true>), g, dim3(TPB), 0, s, c, a, lde, a.dinv, comp));
+}
+
+void launch_lin_lincomb(Prof& prof, hipStream_t s, bool trans, bool two, const felt* coef, uint32_t W, uint32_t logn,
+                        uint64_t p0, uint64_t np, const felt* coefs, const felt* twn, felt* out) {
+  const dim3 g(blocks_for((np + LIN_CH - 1) / LIN_CH));
+  const double bytes = (double)np * 16.0 * (W + (trans ? 1 : 0) + 1 + (two ? 1 : 0));
+#define ZKP_LINC(T, O)                                                                                      \
+  LAUNCH(prof, "lin_lincomb", s, bytes,                                                                     \
+         hipLaunchKernelGGL((k_lin_lincomb<T, O>), g, dim3(TPB), 0, s, coef, W, logn, p0, np, coefs, twn, out))
+  if (trans && two) ZKP_LINC(true, true);
+  else if (trans) ZKP_LINC(true, false);
+  else if (two) ZKP_LINC(false, true);
+  else ZKP_LINC(false, false);
+#undef ZKP_LINC
+}
+
+void launch_eval_linear_pts(Prof& prof, hipStream_t s, const EvalCommon& c, const LinearEvalArgs& a, const felt* ev,
+                            felt* comp) {
+  uint64_t M = (uint64_t)c.cel << c.logn;
+  const bool two = a.two_groups, trans = a.transition;
+  if (!a.binv_ready) launch_den_table(prof, s, c.pm, M, a.w_bstep, a.w_bstep1, two ? 1 : 0, a.binv, a.dinv);
+  const dim3 g(blocks_for((M + LIN_CH - 1) / LIN_CH));
+  const double bytes = (double)M * 16.0 * ((trans ? 1 : 0) + 1 + (two ? 1 : 0) + 2);
+#define ZKP_LINP(T, O)                                                                                      \
+  LAUNCH(prof, "eval_linear", s, bytes,                                                                     \
+         hipLaunchKernelGGL((k_eval_linear_pts<T, O>), g, dim3(TPB), 0, s, c, a, ev, a.dinv, comp))
+  if (trans && two) ZKP_LINP(true, true);
+  else if (trans) ZKP_LINP(true, false);
+  else if (two) ZKP_LINP(false, true);
+  else ZKP_LINP(false, false);
+#undef ZKP_LINP
 }
 
 void launch_eval_bitrev_blocks(Prof& prof, hipStream_t s, const felt* arrays, uint32_t narrays, uint32_t ntwo,

@@ -486,9 +486,15 @@ felt* coset_points(zkp_ctx* ctx, uint32_t logn, uint32_t logB, uint32_t logce) {
 // this rank (its LDE cosets are [j0, j0 + 2^logBl)): composition evaluations
 // comp[ul * n + t] = H(g * w_M^(u0+ul) * w_n^t), i.e. CE domain index (u0+ul) + ce*t.
 // dt_cc = the composition coefficients (device; transition then boundary).
+// Linear AIRs (GlobalUpdate, TrainingUpdate) evaluate in coefficient form when
+// `coef` (the trace coefficient columns) is given (k_lin_lincomb): sharded, every
+// rank of `cm` combines 1/R of the positions and the combined columns are
+// all-gathered, so every rank calls this, with or without CE cosets (cel = 0).
+// ZKP_EVAL_POINTWISE=1 (A/B switch) keeps k_eval_linear over the trace LDE.
 void constraint_eval(zkp_ctx* ctx, const AirDesc& air, uint32_t logn, uint32_t logB, uint32_t logce, uint32_t u0,
                      uint32_t cel, uint32_t j0, uint32_t logBl, const felt* cx, const felt* twn, const felt* dt_cc,
-                     const felt* dt_aval, const felt* tlde, felt* comp) {
+                     const felt* dt_aval, const felt* tlde, felt* comp, const felt* coef = nullptr,
+                     zkp_comm* cm = nullptr) {
   Prof& pf = ctx->prof;
   hipStream_t st = ctx->stream;
   const uint32_t B = 1u << logB, ce = 1u << logce, logN = logn + logB, w = air.w;
@@ -520,6 +526,44 @@ void constraint_eval(zkp_ctx* ctx, const AirDesc& air, uint32_t logn, uint32_t l
   ec.zinv = air.id == ZKP_AIR_MIMC ? dconst : dz;
   const std::string dom = std::to_string(logn) + "_" + std::to_string(logB) + "_" + std::to_string(u0) + "_" +
                           std::to_string(cel);
+  static const bool pointwise = getenv("ZKP_EVAL_POINTWISE") != nullptr;
+  const bool coef_form = air.id != ZKP_AIR_MIMC && coef && !pointwise;
+  if (!cel && !coef_form) return;
+  // linear AIRs: the divisor tables and the final per-point formula (both forms)
+  auto linear = [&](LinearEvalArgs& la, const std::string& key) {
+    la.binv_ready = ctx->have_cached(key);
+    la.binv = ctx->buf<felt>("binv_scratch", ((uint64_t)cel * n) / 2048 + 1);
+    la.dinv = ctx->buf<felt>(key, (uint64_t)cel * n);
+    if (!coef_form) {
+      launch_eval_linear(pf, st, ec, la, tlde, comp);
+      return;
+    }
+    const uint32_t R = cm ? (uint32_t)cm->world : 1u, rank = cm ? (uint32_t)cm->rank : 0u;
+    const uint32_t narr = (la.transition ? 1u : 0u) + 1u + (la.two_groups ? 1u : 0u);
+    const uint64_t nR = n / R;
+    felt* lc = ctx->buf<felt>("lin_coef", (size_t)narr * n);
+    felt* mine = R > 1 ? ctx->buf<felt>("lin_mine", (size_t)narr * nR) : lc;
+    launch_lin_lincomb(pf, st, la.transition, la.two_groups, coef, la.width, logn, (uint64_t)rank * nR, nR,
+                       dconst, twn, mine);
+    for (uint32_t i = 0; R > 1 && i < narr; i++) cm->all_gather(st, mine + i * nR, lc + i * n, nR * 16);
+    if (!cel) return;
+    // extend to the CE cosets u0..u0+cel (LDE cosets u*B/ce): their coset-scale rows
+    // gathered into one table per (n, B, ce), cached
+    const uint32_t cstep = logB - logce;
+    const std::string skey = "Sce_" + std::to_string(logn) + "_" + std::to_string(logB) + "_" + std::to_string(logce);
+    const felt* S = ctx->S(logn, logB);
+    const felt* Sce = S;
+    if (cstep) {
+      felt* t = ctx->buf<felt>(skey, (size_t)ce * n);
+      if (!ctx->have_cached(skey))
+        HIP_CHECK(hipMemcpy2DAsync(t, n * 16, S, (n << cstep) * 16, n * 16, ce, hipMemcpyDeviceToDevice, st));
+      Sce = t;
+    }
+    felt* ev = ctx->buf<felt>("lin_ev", (size_t)narr * cel * n);
+    NttBatch eb{lc, ev, Sce + (uint64_t)u0 * n, n, n, cel, cel, narr * cel};
+    launch_ntt(pf, st, eb, logn, true, ctx->tws(logN), logN);
+    launch_eval_linear_pts(pf, st, ec, la, ev, comp);
+  };
   if (air.id == ZKP_AIR_MIMC) {
     // periodic column K over the CE domain: interpolate over <w_64>, evaluate at g^(n/64) * <w_{64 ce}>
     // (domain-only: cached per (n, ce))
@@ -552,11 +596,7 @@ void constraint_eval(zkp_ctx* ctx, const AirDesc& air, uint32_t logn, uint32_t l
     la.coefs = dconst;  // [next | cur | beta0 | beta1 | bconst0, bconst1]
     la.w_bstep = pow_u64(wn, air.a_step[0]);
     la.w_bstep1 = zero();
-    std::string key = "binv_lin_" + dom + "_" + std::to_string(air.a_step[0]);
-    la.binv_ready = ctx->have_cached(key);
-    la.binv = ctx->buf<felt>("binv_scratch", ((uint64_t)cel * n) / 2048 + 1);
-    la.dinv = ctx->buf<felt>(key, (uint64_t)cel * n);
-    launch_eval_linear(pf, st, ec, la, tlde, comp);
+    linear(la, "binv_lin_" + dom + "_" + std::to_string(air.a_step[0]));
   } else {
     // TrainingUpdate: transitions identically zero; boundary groups at rows 0 and n-1 over
     // the masked columns 0..w/2 (the mask columns are never read)
@@ -568,11 +608,7 @@ void constraint_eval(zkp_ctx* ctx, const AirDesc& air, uint32_t logn, uint32_t l
     la.coefs = dconst;
     la.w_bstep = one();
     la.w_bstep1 = ec.w_last;
-    std::string key = "binv_tu_" + dom;
-    la.binv_ready = ctx->have_cached(key);
-    la.binv = ctx->buf<felt>("binv_scratch", ((uint64_t)cel * n) / 2048 + 1);
-    la.dinv = ctx->buf<felt>(key, (uint64_t)cel * n);
-    launch_eval_linear(pf, st, ec, la, tlde, comp);
+    linear(la, "binv_tu_" + dom);
   }
 }
 
@@ -1122,7 +1158,7 @@ int prove_impl(zkp_ctx* ctx, zkp_comm* cm, int air_id, const felt* d_trace, uint
   // 3. constraint composition coefficients (drawn on the device) + evaluation (DefaultConstraintEvaluator)
   if (!coeffs_drawn) launch_dt_draw_coeffs(pf, st, dt_seed, troot_d, o->batching_constraints, ncoef, dt_cc);
   felt* comp = ctx->buf<felt>("comp", (size_t)(cel ? cel : 1) * n);
-  if (cel) constraint_eval(ctx, air, logn, logB, logce, u0, cel, j0, logBl, cx, twn, dt_cc, dt_aval, tlde, comp);
+  constraint_eval(ctx, air, logn, logB, logce, u0, cel, j0, logBl, cx, twn, dt_cc, dt_aval, tlde, comp, coef, cm);
 
   // 4. composition polynomial + commitment (CompositionPoly::new +
   // DefaultConstraintCommitment): per-CE-coset interpolation, exchange of
@@ -2123,7 +2159,7 @@ int zkp_eval_constraints(zkp_session* s, const zkp_felt* coeffs, uint32_t n_coef
     const felt* twn = ctx->tws(s->logN) + ((1ull << (s->logn - 1)) - 1);
     felt* comp = s->buf<felt>("comp", (size_t)s->ce * s->n);
     constraint_eval(ctx, air, s->logn, s->logB, s->logce, 0, s->ce, 0, s->logB, cx, twn, dcc, daval, s->get("tlde"),
-                    comp);
+                    comp, s->get("coef"));
     if (evals_out) {  // CE-coset-major on the device -> natural CE domain order
       std::vector<felt> h((size_t)s->ce * s->n);
       ctx->download(h.data(), comp, h.size() * 16);

@@ -216,6 +216,15 @@ struct LinearEvalArgs {
 };
 void launch_eval_linear(Prof& prof, hipStream_t s, const EvalCommon& c, const LinearEvalArgs& a, const felt* lde,
                         felt* comp);
+// the same in coefficient form (kernels.hip, k_lin_lincomb): the coefficients of
+// [A (trans) | B0 | B1 (two)] over bit-reversed positions [p0, p0 + np) of the
+// first W coefficient columns (out: np felts per array; twn[j] = w_n^j, j < n/2),
+// then, once they are extended to the shard's CE cosets (ev: cel*n per array),
+// the per-point formula of k_eval_linear
+void launch_lin_lincomb(Prof& prof, hipStream_t s, bool trans, bool two, const felt* coef, uint32_t W, uint32_t logn,
+                        uint64_t p0, uint64_t np, const felt* coefs, const felt* twn, felt* out);
+void launch_eval_linear_pts(Prof& prof, hipStream_t s, const EvalCommon& c, const LinearEvalArgs& a, const felt* ev,
+                            felt* comp);
 
 // composition polynomial from CE-coset interpolations (see kernels.hip): for the
 // bit-reversed positions [p0, p0 + nR), n * c_m = (sum_u Si_u * W_u * w_ce^-um) * g^-mn / ce;
