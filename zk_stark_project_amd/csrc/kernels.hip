@@ -407,18 +407,30 @@ __global__ __launch_bounds__(TPB) void k_eval_linear(EvalCommon c, LinearEvalArg
 // them to its CE cosets and k_eval_linear_pts applies k_eval_linear's final
 // formula point by point: the same field values.
 // out = [A (TRANS) | B0 | B1 (TWO)], np felts each; twn[j] = w_n^j (j < n/2).
-template <bool TRANS, bool TWO>
+// Column groups (blockIdx.y, cpg columns each) keep small position ranges (a
+// rank's 1/R slice) from running a few waves per CU: with PART each group writes
+// its partial sums [sa | sb | s0 | s1] (np each) to out + 4*np*group and
+// k_lin_reduce adds the groups and applies the final formula.
+__device__ __forceinline__ felt lin_finish_a(uint64_t p, uint32_t logn, const felt* twn, felt sa, felt sb) {
+  const uint64_t n = 1ull << logn;
+  const uint64_t d = __brevll(p) >> (64 - logn);  // the coefficient's degree
+  const felt wd = d < (n >> 1) ? twn[d] : neg(twn[d - (n >> 1)]);
+  return add(mul(wd, sa), sb);
+}
+template <bool TRANS, bool TWO, bool PART>
 __global__ __launch_bounds__(TPB) void k_lin_lincomb(const felt* __restrict__ coef, uint32_t W, uint32_t logn,
                                                      uint64_t p0, uint64_t np, const felt* __restrict__ coefs,
-                                                     const felt* __restrict__ twn, felt* __restrict__ out) {
+                                                     const felt* __restrict__ twn, uint32_t cpg,
+                                                     felt* __restrict__ out) {
   const uint64_t n = 1ull << logn;
+  const uint32_t c0 = blockIdx.y * cpg, c1 = c0 + cpg < W ? c0 + cpg : W;
   felt sa[LIN_CH], sb[LIN_CH], s0[LIN_CH], s1[LIN_CH];
   uint64_t p[LIN_CH];
   static_for<0, LIN_CH>([&](auto k) {
     p[k] = p0 + (LIN_POINT(k) < np ? LIN_POINT(k) : 0);
     sa[k] = zero(); sb[k] = zero(); s0[k] = zero(); s1[k] = zero();
   });
-  for (uint32_t c = 0; c < W; c++) {
+  for (uint32_t c = c0; c < c1; c++) {
     const felt* col = coef + (uint64_t)c * n;
     felt v[LIN_CH];
     static_for<0, LIN_CH>([&](auto k) { v[k] = col[p[k]]; });
@@ -436,16 +448,42 @@ __global__ __launch_bounds__(TPB) void k_lin_lincomb(const felt* __restrict__ co
   static_for<0, LIN_CH>([&](auto k) {
     const uint64_t i = LIN_POINT(k);
     if (i >= np) return;
+    if (PART) {
+      felt* o = out + (uint64_t)blockIdx.y * 4 * np + i;
+      if (TRANS) { o[0] = sa[k]; o[np] = sb[k]; }
+      o[2 * np] = s0[k];
+      if (TWO) o[3 * np] = s1[k];
+      return;
+    }
     felt* o = out + i;
     if (TRANS) {
-      const uint64_t d = __brevll(p[k]) >> (64 - logn);  // the coefficient's degree
-      const felt wd = d < (n >> 1) ? twn[d] : neg(twn[d - (n >> 1)]);
-      *o = add(mul(wd, sa[k]), sb[k]);
+      *o = lin_finish_a(p[k], logn, twn, sa[k], sb[k]);
       o += np;
     }
     *o = s0[k];
     if (TWO) o[np] = s1[k];
   });
+}
+template <bool TRANS, bool TWO>
+__global__ __launch_bounds__(TPB) void k_lin_reduce(const felt* __restrict__ part, uint32_t G, uint32_t logn,
+                                                    uint64_t p0, uint64_t np, const felt* __restrict__ twn,
+                                                    felt* __restrict__ out) {
+  const uint64_t i = blockIdx.x * (uint64_t)TPB + threadIdx.x;
+  if (i >= np) return;
+  felt sa = zero(), sb = zero(), s0 = zero(), s1 = zero();
+  for (uint32_t g = 0; g < G; g++) {
+    const felt* q = part + (uint64_t)g * 4 * np + i;
+    if (TRANS) { sa = add(sa, q[0]); sb = add(sb, q[np]); }
+    s0 = add(s0, q[2 * np]);
+    if (TWO) s1 = add(s1, q[3 * np]);
+  }
+  felt* o = out + i;
+  if (TRANS) {
+    *o = lin_finish_a(p0 + i, logn, twn, sa, sb);
+    o += np;
+  }
+  *o = s0;
+  if (TWO) o[np] = s1;
 }
 
 // k_eval_linear's final formula over the extended arrays ev = [A | B0 | B1]
@@ -659,25 +697,37 @@ __global__ __launch_bounds__(TPB) void k_deep(DeepArgs a, const felt* __restrict
 // apart; column-outer so each column's loads are in flight together. Its coset
 // LDE then replaces w column reads per LDE point of the pointwise k_deep by one.
 // A rank of a sharded proof combines the positions [p0, p0 + np) (out[0, np)).
+template <bool PART>
 __global__ __launch_bounds__(TPB) void k_deep_lincomb(const felt* __restrict__ coef, uint32_t w, uint64_t n,
                                                       uint64_t p0, uint64_t np, const felt* __restrict__ gamma,
-                                                      felt* __restrict__ out) {
+                                                      uint32_t cpg, felt* __restrict__ out) {
+  const uint32_t c0 = blockIdx.y * cpg, c1 = c0 + cpg < w ? c0 + cpg : w;
   felt acc[LIN_CH];
   uint64_t p[LIN_CH];
   static_for<0, LIN_CH>([&](auto k) {
     p[k] = p0 + (LIN_POINT(k) < np ? LIN_POINT(k) : 0);
     acc[k] = zero();
   });
-  for (uint32_t c = 0; c < w; c++) {
+  for (uint32_t c = c0; c < c1; c++) {
     const felt g = gamma[c];
     const felt* col = coef + (uint64_t)c * n;
     felt v[LIN_CH];
     static_for<0, LIN_CH>([&](auto k) { v[k] = col[p[k]]; });
     static_for<0, LIN_CH>([&](auto k) { acc[k] = add(acc[k], mul(g, v[k])); });
   }
+  felt* o = out + (PART ? (uint64_t)blockIdx.y * np : 0);
   static_for<0, LIN_CH>([&](auto k) {
-    if (LIN_POINT(k) < np) out[LIN_POINT(k)] = acc[k];
+    if (LIN_POINT(k) < np) o[LIN_POINT(k)] = acc[k];
   });
+}
+// out[i] = sum_g part[g*np + i]
+__global__ __launch_bounds__(TPB) void k_sum_groups(const felt* __restrict__ part, uint32_t G, uint64_t np,
+                                                    felt* __restrict__ out) {
+  const uint64_t i = blockIdx.x * (uint64_t)TPB + threadIdx.x;
+  if (i >= np) return;
+  felt a = part[i];
+  for (uint32_t g = 1; g < G; g++) a = add(a, part[(uint64_t)g * np + i]);
+  out[i] = a;
 }
 
 // multi-segment gather: segment s copies seg[s].count items of seg[s].words
@@ -891,17 +941,37 @@ void launch_eval_linear(Prof& prof, hipStream_t s, const EvalCommon& c, const Li
            hipLaunchKernelGGL((k_eval_linear<true, true>), g, dim3(TPB), 0, s, c, a, lde, a.dinv, comp));
 }
 
+uint32_t lincomb_groups(uint64_t np, uint32_t W) {
+  const uint64_t waves = ((np + LIN_CH - 1) / LIN_CH + 63) / 64;
+  uint64_t G = (4096 + waves - 1) / waves;  // aim at >= 4 waves per SIMD
+  const uint64_t gmax = W >= 8 ? W / 4 : 1;  // >= 4 columns per group
+  if (G > gmax) G = gmax;
+  if (G > 16) G = 16;
+  return G ? (uint32_t)G : 1u;
+}
+
 void launch_lin_lincomb(Prof& prof, hipStream_t s, bool trans, bool two, const felt* coef, uint32_t W, uint32_t logn,
-                        uint64_t p0, uint64_t np, const felt* coefs, const felt* twn, felt* out) {
-  const dim3 g(blocks_for((np + LIN_CH - 1) / LIN_CH));
+                        uint64_t p0, uint64_t np, const felt* coefs, const felt* twn, felt* out, felt* scratch) {
+  const uint32_t G = scratch ? lincomb_groups(np, W) : 1u, cpg = (W + G - 1) / G;
+  const dim3 g(blocks_for((np + LIN_CH - 1) / LIN_CH), G);
   const double bytes = (double)np * 16.0 * (W + (trans ? 1 : 0) + 1 + (two ? 1 : 0));
-#define ZKP_LINC(T, O)                                                                                      \
-  LAUNCH(prof, "lin_lincomb", s, bytes,                                                                     \
-         hipLaunchKernelGGL((k_lin_lincomb<T, O>), g, dim3(TPB), 0, s, coef, W, logn, p0, np, coefs, twn, out))
-  if (trans && two) ZKP_LINC(true, true);
-  else if (trans) ZKP_LINC(true, false);
-  else if (two) ZKP_LINC(false, true);
-  else ZKP_LINC(false, false);
+#define ZKP_LINC(T, O)                                                                                          \
+  if (G == 1)                                                                                                   \
+    LAUNCH(prof, "lin_lincomb", s, bytes,                                                                       \
+           hipLaunchKernelGGL((k_lin_lincomb<T, O, false>), g, dim3(TPB), 0, s, coef, W, logn, p0, np, coefs, twn, \
+                              cpg, out));                                                                       \
+  else {                                                                                                        \
+    LAUNCH(prof, "lin_lincomb", s, bytes,                                                                       \
+           hipLaunchKernelGGL((k_lin_lincomb<T, O, true>), g, dim3(TPB), 0, s, coef, W, logn, p0, np, coefs, twn,  \
+                              cpg, scratch));                                                                   \
+    LAUNCH(prof, "lin_lincomb", s, (double)np * 16.0 * 4 * G,                                                  \
+           hipLaunchKernelGGL((k_lin_reduce<T, O>), dim3(blocks_for(np)), dim3(TPB), 0, s, scratch, G, logn, p0,  \
+                              np, twn, out));                                                                   \
+  }
+  if (trans && two) { ZKP_LINC(true, true) }
+  else if (trans) { ZKP_LINC(true, false) }
+  else if (two) { ZKP_LINC(false, true) }
+  else { ZKP_LINC(false, false) }
 #undef ZKP_LINC
 }
 
@@ -955,10 +1025,18 @@ void launch_deep_denominators(Prof& prof, hipStream_t s, const PointMap& m, uint
 }
 
 void launch_deep_lincomb(Prof& prof, hipStream_t s, const felt* coef, uint32_t w, uint64_t n, uint64_t p0,
-                         uint64_t np, const felt* gamma, felt* out) {
+                         uint64_t np, const felt* gamma, felt* out, felt* scratch) {
+  const uint32_t G = scratch ? lincomb_groups(np, w) : 1u, cpg = (w + G - 1) / G;
+  const dim3 g(blocks_for((np + LIN_CH - 1) / LIN_CH), G);
+  if (G == 1) {
+    LAUNCH(prof, "deep_lincomb", s, (double)(w + 1) * np * 16.0,
+           hipLaunchKernelGGL(k_deep_lincomb<false>, g, dim3(TPB), 0, s, coef, w, n, p0, np, gamma, cpg, out));
+    return;
+  }
   LAUNCH(prof, "deep_lincomb", s, (double)(w + 1) * np * 16.0,
-         hipLaunchKernelGGL(k_deep_lincomb, dim3(blocks_for((np + LIN_CH - 1) / LIN_CH)), dim3(TPB), 0, s, coef, w, n,
-                            p0, np, gamma, out));
+         hipLaunchKernelGGL(k_deep_lincomb<true>, g, dim3(TPB), 0, s, coef, w, n, p0, np, gamma, cpg, scratch));
+  LAUNCH(prof, "deep_lincomb", s, (double)(G + 1) * np * 16.0,
+         hipLaunchKernelGGL(k_sum_groups, dim3(blocks_for(np)), dim3(TPB), 0, s, scratch, G, np, out));
 }
 
 void launch_deep(Prof& prof, hipStream_t s, const DeepArgs& a, felt* out) {

@@ -70,12 +70,14 @@ __global__ __launch_bounds__(1024) void k_merkle_top(uint32_t* nodes, uint64_t s
 // held in LDS and every node written once to nodes[] (tree layout: level d of
 // an L-leaf tree at nodes[(L >> d) .. (2L >> d))). MODE 0: leaves = rows of a
 // coset-major LDE matrix; MODE 1: leaves = FRI rows [E[r + k*R]]; MODE 2:
-// leaves already stored in nodes[L..2L).
+// leaves already stored in nodes[L..2L); MODE 3: leaf digests in a sharded
+// commitment's all-to-all receive buffer (src; k_leaf_unpack's layout), stored
+// to nodes[L..2L) on the way up.
 struct MerkleArgs {
   const felt* src;
   uint64_t n;       // MODE 0: rows per coset
-  uint32_t cols;    // MODE 0: columns; MODE 1: F
-  uint32_t logB;    // MODE 0/1: cosets of the (coset-major) source
+  uint32_t cols;    // MODE 0: columns; MODE 1: F; MODE 3: log2 rows per chunk and source (logrc)
+  uint32_t logB;    // MODE 0/1/3: cosets of the (coset-major) source
   uint64_t R;       // MODE 1: rows per coset (m/16)
   uint32_t* nodes;
   uint64_t L;       // leaves of this (sub)tree level
@@ -93,6 +95,11 @@ __device__ __forceinline__ void merkle_leaf(const MerkleArgs& a, uint64_t i, uin
     // natural row i = j + B*t' -> coset j, positions t' + k*R
     const felt* base = a.src + ((i & ((1ull << a.logB) - 1)) * 16) * a.R + (i >> a.logB);
     b3::hash_felts([&](uint32_t k) { return base[k * a.R]; }, a.cols, d);
+  } else if (MODE == 3) {
+    // leaf i = j + B*tl sits in chunk k = tl >> logrc, source block j, row tl mod rc
+    const uint64_t j = i & ((1ull << a.logB) - 1), tl = i >> a.logB;
+    const uint64_t k = tl >> a.cols, tc = tl & ((1ull << a.cols) - 1);
+    load_digest(reinterpret_cast<const uint32_t*>(a.src) + (((k << a.logB) + j) << a.cols | tc) * 8, d);
   } else {
     load_digest(a.nodes + (a.L + i) * 8, d);
   }
@@ -1376,9 +1383,47 @@ void launch_leaf_hash_shard(Prof& prof, hipStream_t s, int mode, const felt* src
 void launch_merkle_from_shards(Prof& prof, hipStream_t s, const uint32_t* recv, uint32_t logB, uint32_t logrr,
                                uint32_t logK, uint32_t* nodes) {
   const uint64_t L = 1ull << (logB + logrr);
-  LAUNCH(prof, "leaf_unpack", s, (double)L * 64.0,
-         hipLaunchKernelGGL(k_leaf_unpack, dim3(blocks_for(L)), dim3(TPB), 0, s, recv, logB, logrr, logK, nodes, L));
-  merkle_upper(prof, s, nodes, L, nullptr);
+  static const bool separate = getenv("ZKP_LEAF_UNPACK") != nullptr;  // A/B switch: the unfused unpack pass
+  if (separate || L < 4) {
+    LAUNCH(prof, "leaf_unpack", s, (double)L * 64.0,
+           hipLaunchKernelGGL(k_leaf_unpack, dim3(blocks_for(L)), dim3(TPB), 0, s, recv, logB, logrr, logK, nodes, L));
+    merkle_upper(prof, s, nodes, L, nullptr);
+    return;
+  }
+  // the unpack fused into the first 2-level lane pass: each lane loads its 4 leaf
+  // digests from the receive buffer, stores them as leaves and merges 2 levels
+  MerkleArgs a{};
+  a.src = reinterpret_cast<const felt*>(recv);
+  a.cols = logrr - logK;
+  a.logB = logB;
+  a.nodes = nodes;
+  a.L = L;
+  merkle_pass<3>(prof, s, a, 2, "merkle_upper", (double)L * 32.0 * 2.5);
+  merkle_upper(prof, s, nodes, L >> 2, nullptr);
+}
+
+// top levels of a sharded tree from the all-gathered subtree roots (R <= 64):
+// top[R + s] = root of rank s's subtree, top[k] = merge(top[2k], top[2k+1]);
+// the root (top[1]) stays on the device for the coin kernels
+__global__ __launch_bounds__(64) void k_shard_top(const uint32_t* __restrict__ roots, uint32_t R,
+                                                  uint32_t* __restrict__ top) {
+  const uint32_t t = threadIdx.x;
+  if (t < R)
+    for (int i = 0; i < 8; i++) top[(R + t) * 8 + i] = roots[t * 8 + i];
+  for (uint32_t h = R >> 1; h >= 1; h >>= 1) {
+    __syncthreads();
+    if (t < h) {
+      uint32_t l[8], r[8], o[8];
+      load_digest(top + (2 * (h + t)) * 8, l);
+      load_digest(top + (2 * (h + t) + 1) * 8, r);
+      merge8<true>(l, r, o);
+      store_digest(top + (h + t) * 8, o);
+    }
+  }
+}
+
+void launch_shard_top(Prof& prof, hipStream_t s, const uint32_t* roots, uint32_t R, uint32_t* top) {
+  LAUNCH(prof, "merkle_top9", s, (double)R * 64.0, hipLaunchKernelGGL(k_shard_top, dim3(1), dim3(64), 0, s, roots, R, top));
 }
 
 void launch_dt_draw_coeffs(Prof& prof, hipStream_t s, uint32_t* seed, const uint32_t* root, uint32_t method,

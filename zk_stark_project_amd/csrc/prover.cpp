@@ -314,6 +314,7 @@ struct TreeShard {
   uint64_t Lr = 0;
   uint32_t logR = 0;
   std::vector<std::array<uint8_t, 32>> top;
+  uint32_t* top_d = nullptr;  // sharded: top[1..2R) on the device (root at top_d + 8)
   // global node k -> host digest (top levels) or (owner rank, local node index)
   struct Loc {
     bool host;
@@ -367,7 +368,8 @@ bool commit_rows(zkp_ctx* ctx, zkp_comm* cm, int mode, const felt* src, uint64_t
   // the leaf-digest all-to-all in K chunks on the side stream, chunk k's exchange
   // overlapping the hashing of chunk k+1 (every hash launch is queued before the
   // first collective, so host-synchronous transports overlap too)
-  const uint32_t logK = logrr >= 12 ? 2u : 0u, K = 1u << logK;
+  static const int logK_env = getenv("ZKP_SHARD_LOGK") ? atoi(getenv("ZKP_SHARD_LOGK")) : -1;  // A/B switch
+  const uint32_t logK = logrr >= 12 ? (logK_env >= 0 && logK_env <= 4 ? (uint32_t)logK_env : 2u) : 0u, K = 1u << logK;
   const size_t chunk_words = (size_t)8 << (logBl + logrows - logK), block = (size_t)32 << (logBl + logrr - logK);
   ctx->events(K + 1);
   for (uint32_t k = 0; k < K; k++) {
@@ -382,14 +384,18 @@ bool commit_rows(zkp_ctx* ctx, zkp_comm* cm, int mode, const felt* src, uint64_t
   HIP_CHECK(hipStreamWaitEvent(st, ctx->up_ev[K], 0));
   tr.nodes = ctx->buf<uint32_t>(name, (size_t)16 * tr.Lr);
   launch_merkle_from_shards(pf, st, recv, logB, logrr, logK, tr.nodes);
+  // the top levels on the device from the all-gathered subtree roots: the coin
+  // kernels read the root there, and the host fetches tr.top with the transcript
+  // (fetch_root = false) instead of a round trip per commitment
   uint32_t* roots = ctx->buf<uint32_t>("shard_roots", (size_t)8 * R);
   cm->all_gather(st, tr.nodes + 8, roots, 32);
-  std::vector<uint8_t> hr((size_t)32 * R);
-  ctx->download(hr.data(), roots, hr.size());
+  tr.top_d = ctx->buf<uint32_t>(name + "_top", (size_t)16 * R);
+  launch_shard_top(pf, st, roots, R, tr.top_d);
   tr.top.assign(2 * R, {});
-  for (uint32_t s = 0; s < R; s++) memcpy(tr.top[R + s].data(), hr.data() + 32 * s, 32);
-  for (uint32_t k = R - 1; k >= 1; k--) merge_bytes(tr.top[2 * k].data(), tr.top[2 * k + 1].data(), tr.top[k].data());
-  memcpy(root, tr.top[1].data(), 32);
+  if (fetch_root) {
+    ctx->download(tr.top.data(), tr.top_d, (size_t)64 * R);
+    memcpy(root, tr.top[1].data(), 32);
+  }
   return false;
 }
 
@@ -543,8 +549,9 @@ void constraint_eval(zkp_ctx* ctx, const AirDesc& air, uint32_t logn, uint32_t l
     const uint64_t nR = n / R;
     felt* lc = ctx->buf<felt>("lin_coef", (size_t)narr * n);
     felt* mine = R > 1 ? ctx->buf<felt>("lin_mine", (size_t)narr * nR) : lc;
+    felt* part = ctx->buf<felt>("lincomb_part", (size_t)4 * lincomb_groups(nR, la.width) * nR);
     launch_lin_lincomb(pf, st, la.transition, la.two_groups, coef, la.width, logn, (uint64_t)rank * nR, nR,
-                       dconst, twn, mine);
+                       dconst, twn, mine, part);
     for (uint32_t i = 0; R > 1 && i < narr; i++) cm->all_gather(st, mine + i * nR, lc + i * n, nR * 16);
     if (!cel) return;
     // extend to the CE cosets u0..u0+cel (LDE cosets u*B/ce): their coset-scale rows
@@ -643,12 +650,13 @@ void deep_evaluations(zkp_ctx* ctx, zkp_comm* cm, hipStream_t st, DeepArgs da, c
   const uint32_t Bl = 1u << da.logBl;
   const uint32_t R = (uint32_t)cm->world;
   felt* acomb = ctx->buf<felt>("deep_acoef", n);
+  const uint64_t nR = n / R;
+  felt* part = ctx->buf<felt>("lincomb_part", (size_t)lincomb_groups(nR, da.w) * nR);
   if (R == 1) {
-    launch_deep_lincomb(ctx->prof, st, coef, da.w, n, 0, n, da.gamma, acomb);
+    launch_deep_lincomb(ctx->prof, st, coef, da.w, n, 0, n, da.gamma, acomb, part);
   } else {
-    const uint64_t nR = n / R;
     felt* mine = ctx->buf<felt>("deep_acoef_rank", nR);
-    launch_deep_lincomb(ctx->prof, st, coef, da.w, n, (uint64_t)cm->rank * nR, nR, da.gamma, mine);
+    launch_deep_lincomb(ctx->prof, st, coef, da.w, n, (uint64_t)cm->rank * nR, nR, da.gamma, mine, part);
     cm->all_gather(st, mine, acomb, nR * 16);
   }
   felt* alde = ctx->buf<felt>("deep_alde", (size_t)Bl * n);
@@ -1027,7 +1035,6 @@ int prove_impl(zkp_ctx* ctx, zkp_comm* cm, int air_id, const felt* d_trace, uint
   // host replays both draws from the downloaded roots and checks them
   const uint32_t ncoef = air.num_t + (uint32_t)air.a_col.size();
   uint32_t* dt_seed = ctx->buf<uint32_t>("dt_seed", 8);
-  uint32_t* dt_roots = ctx->buf<uint32_t>("dt_roots", 16);  // staged roots of sharded commitments
   felt* dt_cc = ctx->buf<felt>("dt_cc", ncoef);
   felt* dt_zz = ctx->buf<felt>("dt_zz", 2);
   felt* dt_pw = ctx->buf<felt>("dt_pw", 2 * (size_t)logn);
@@ -1146,13 +1153,9 @@ int prove_impl(zkp_ctx* ctx, zkp_comm* cm, int air_id, const felt* d_trace, uint
     draw.ncoef = ncoef;
     draw.out = dt_cc;
     coeffs_drawn = commit_rows(ctx, cm, 0, tlde, n, w, logB, logn, R > 1, "ttree", ttree, T.trace_root,
-                               /*fetch_root=*/R > 1, &draw);
+                               /*fetch_root=*/false, &draw);
   }
-  const uint32_t* troot_d = ttree.nodes + 8;
-  if (R > 1) {  // sharded: the root was assembled on the host from the subtree roots
-    ctx->upload(dt_roots, T.trace_root, 32);
-    troot_d = dt_roots;
-  }
+  const uint32_t* troot_d = R > 1 ? ttree.top_d + 8 : ttree.nodes + 8;  // sharded: the device-built top
   ctx->stage_end("1_trace_commit");
 
   // 3. constraint composition coefficients (drawn on the device) + evaluation (DefaultConstraintEvaluator)
@@ -1231,13 +1234,9 @@ int prove_impl(zkp_ctx* ctx, zkp_comm* cm, int air_id, const felt* d_trace, uint
     draw.out = dt_zz;
     draw.pw = dt_pw;
     z_drawn = commit_rows(ctx, cm, 0, clde, n, C, logB, logn, R > 1, "ctree", ctree, T.constraint_root,
-                          /*fetch_root=*/R > 1, &draw);
+                          /*fetch_root=*/false, &draw);
   }
-  const uint32_t* croot_d = ctree.nodes + 8;
-  if (R > 1) {
-    ctx->upload(dt_roots + 8, T.constraint_root, 32);
-    croot_d = dt_roots + 8;
-  }
+  const uint32_t* croot_d = R > 1 ? ctree.top_d + 8 : ctree.nodes + 8;
   if (!z_drawn) launch_dt_draw_z(pf, st, dt_seed, croot_d, wn_root, logn, dt_zz, dt_pw);
   ctx->stage_end("2_constraints_commit");
 
@@ -1362,16 +1361,10 @@ int prove_impl(zkp_ctx* ctx, zkp_comm* cm, int air_id, const felt* d_trace, uint
       coin.alpha_out = alphas_d + l;
       coin.root_out = roots_d + 8 * (size_t)l;
       const bool coin_done = commit_rows(ctx, cm, 1, E, 0, F, logB, ilog2(m16), sh, "ftree_" + std::to_string(l),
-                                         ly.tree, T.fri_roots[l], /*fetch_root=*/sh, &coin);
-      if (!coin_done) {
-        const uint32_t* root_src = ly.tree.nodes + 8;
-        if (sh) {
-          uint32_t* staged = roots_d + 8 * (size_t)L;  // scratch slot
-          ctx->upload(staged, T.fri_roots[l], 32);
-          root_src = staged;
-        }
-        launch_coin_fri_layer(pf, st, coin_d, root_src, alphas_d + l, roots_d + 8 * (size_t)l);
-      }
+                                         ly.tree, T.fri_roots[l], /*fetch_root=*/false, &coin);
+      if (!coin_done)
+        launch_coin_fri_layer(pf, st, coin_d, sh ? ly.tree.top_d + 8 : ly.tree.nodes + 8, alphas_d + l,
+                              roots_d + 8 * (size_t)l);
       felt* nxt = fe + eo;
       launch_fri_fold(pf, st, E, m16, Bc, jc, logB, F, alphas_d + l, inv(off), ctx->itws(logN), ilog2(D), deps,
                       nxt);
@@ -1466,6 +1459,11 @@ int prove_impl(zkp_ctx* ctx, zkp_comm* cm, int air_id, const felt* d_trace, uint
       fs.push_back({raw_pos.data(), dpos, raw_pos.size() * 8});
       fs.push_back({full_h.data(), full_d, full_h.size() * 4});
     }
+    // sharded trees: their device-built top levels (the openings' host part)
+    for (TreeShard* t : {&ttree, &ctree})
+      if (t->top_d) fs.push_back({t->top.data(), t->top_d, t->top.size() * 32});
+    for (uint32_t l = 0; l < L; l++)
+      if (layers[l].tree.top_d) fs.push_back({layers[l].tree.top.data(), layers[l].tree.top_d, layers[l].tree.top.size() * 32});
     fetch_all(ctx, fs);
     memcpy(T.trace_root, roots, 32);
     memcpy(T.constraint_root, roots + 32, 32);

@@ -100,6 +100,8 @@ bool merkle_upper(Prof& prof, hipStream_t s, uint32_t* nodes, uint64_t L, const 
 void launch_leaf_hash_shard(Prof& prof, hipStream_t s, int mode, const felt* src, uint64_t n, uint32_t cols,
                             uint32_t logBl, uint32_t logrows, uint32_t logrr, uint32_t logK, uint32_t k,
                             uint32_t* send);
+// sharded tree tops (R <= 64 subtree roots, all-gathered) -> top[1..2R) on the device
+void launch_shard_top(Prof& prof, hipStream_t s, const uint32_t* roots, uint32_t R, uint32_t* top);
 void launch_merkle_from_shards(Prof& prof, hipStream_t s, const uint32_t* recv, uint32_t logB, uint32_t logrr,
                                uint32_t logK, uint32_t* nodes);
 // internal nodes nodes[1..L) from leaves nodes[L..2L)
@@ -221,8 +223,11 @@ void launch_eval_linear(Prof& prof, hipStream_t s, const EvalCommon& c, const Li
 // first W coefficient columns (out: np felts per array; twn[j] = w_n^j, j < n/2),
 // then, once they are extended to the shard's CE cosets (ev: cel*n per array),
 // the per-point formula of k_eval_linear
+// Small position ranges split the columns into lincomb_groups(np, W) groups
+// (partial sums in `scratch`: 4 * np felts per group, nullable = one group).
+uint32_t lincomb_groups(uint64_t np, uint32_t W);
 void launch_lin_lincomb(Prof& prof, hipStream_t s, bool trans, bool two, const felt* coef, uint32_t W, uint32_t logn,
-                        uint64_t p0, uint64_t np, const felt* coefs, const felt* twn, felt* out);
+                        uint64_t p0, uint64_t np, const felt* coefs, const felt* twn, felt* out, felt* scratch);
 void launch_eval_linear_pts(Prof& prof, hipStream_t s, const EvalCommon& c, const LinearEvalArgs& a, const felt* ev,
                             felt* comp);
 
@@ -267,7 +272,8 @@ void launch_deep(Prof& prof, hipStream_t s, const DeepArgs& a, felt* out);
 // before extending): out[p] = sum_{c < w} gamma[c] * coef[c*n + p]
 // over the bit-reversed, n-scaled coefficient columns -> one combined column (same layout)
 void launch_deep_lincomb(Prof& prof, hipStream_t s, const felt* coef, uint32_t w, uint64_t n, uint64_t p0,
-                         uint64_t np, const felt* gamma, felt* out);  // positions [p0, p0 + np) -> out[0, np)
+                         uint64_t np, const felt* gamma, felt* out,  // positions [p0, p0 + np) -> out[0, np)
+                         felt* scratch);  // column-group partials (np per group, see lincomb_groups), nullable
 
 // FRI fold-by-F (F = 16) over coset-major evaluations of the cosets [j0, j0+Bl)
 // (16*m16 positions each): natural row r = j + B*t', x_r = off * w_D^r; alpha read from device
