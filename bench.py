@@ -50,7 +50,8 @@ E, H = 16, 32  # felt and digest bytes
 # summaries that scripts/profile_round.sh writes (profiles/r0*_pmc_*.json)
 KERNEL_SYMBOL = {
     "ntt_dit": "void k_ntt8<true,", "ntt_dif": "void k_ntt8<false,", "deep": "k_deep",
-    "merkle_lde": "void k_merkle_lane<0,", "eval_mimc": "k_eval_mimc", "eval_linear": "void k_eval_linear<",
+    "merkle_lde": ("void k_merkle_lane<0,", "void k_merkle_leaf2<"), "eval_mimc": "k_eval_mimc",
+    "eval_linear": ("void k_eval_linear<", "void k_eval_linear_pts<"),
 }
 # launch name -> SURVEY.md Appendix C stages whose algorithmic bytes that kernel moves
 KERNEL_STAGES = {
@@ -93,7 +94,7 @@ def load_pmc(kind: str, air: str, kernel: str):
     if not prefix or not os.path.exists(path):
         return None, name
     with open(path) as f:
-        recs = {k: v for k, v in json.load(f).items() if k == prefix or k.startswith(prefix)}
+        recs = {k: v for k, v in json.load(f).items() if k.startswith(prefix)}  # prefix: str or tuple of str
     if not sum(v["launches"] for v in recs.values()):
         return None, name
     return recs, name
