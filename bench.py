@@ -542,6 +542,11 @@ def main():
         "first_proof_ms": round(first_ms, 3),
         "sustained": {"proofs": sus_n, "seconds": round(sus_s, 3), "proofs_per_s": round(sus_n / sus_s, 3)},
         "roofline": roofline,
+        # every launch of the two profiled proofs (HIP events per launch, side stream included)
+        "launches": {"per_proof": sum(v["launches"] for v in kernels.values()) / 2,
+                     "kernel_ms_per_proof": round(total_ms / 2, 3),
+                     "by_kernel_ms": {k: round(v["ms"] / 2, 4) for k, v in
+                                      sorted(kernels.items(), key=lambda kv: -kv[1]["ms"])}},
         "cpu_baseline": cpu,
         "c1": c1,
         "proof_bytes": len(proof),
