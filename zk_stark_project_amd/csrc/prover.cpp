@@ -978,53 +978,140 @@ const felt* fold_constants(zkp_ctx* ctx) {
   return deps;
 }
 
-// h_trace (nullable): the trace is still in host memory and d_trace is its
-// device buffer; the upload is pipelined with the trace interpolation and LDE
-// by column groups (wide traces), so PCIe overlaps the first stage's kernels.
-int prove_impl(zkp_ctx* ctx, zkp_comm* cm, int air_id, const felt* d_trace, uint32_t w, uint64_t n,
-               const zkp_felt* pub_elems, uint64_t n_pub, const zkp_proof_options* o, uint8_t** proof,
-               uint64_t* proof_len, zkp_transcript* tr_out, const zkp_felt* h_trace = nullptr) {
+// where the FRI layer loop left off: the last layer (E: m per coset, D values
+// in all, domain offset off) and the device coin / alphas / roots
+struct FriCursor {
+  felt* E;
+  uint64_t m, D;
+  felt off;
+  uint32_t* coin_d;
+  felt* alphas_d;
+  uint32_t* roots_d;
+};
+
+// One proof (prove_impl): the shapes, device buffers, commitments and transcript
+// that its stages share. Each stage method is one step of the reference's
+// Prover::prove (winter-prover 0.12 generate_proof); what a later
+// step reads is a member, everything else stays local to its stage.
+struct ProofRun {
+  zkp_ctx* ctx;
+  zkp_comm* cm;
+  const zkp_proof_options* o;
+  hipStream_t st;
+  Prof& pf;
+  // shapes; coset sharding: rank r owns the LDE cosets [j0, j0 + Bl)
+  uint32_t w = 0, B = 0, F = 0, logn = 0, logB = 0, logN = 0, R = 1, rank = 0, logR = 0, Bl = 0, logBl = 0, j0 = 0;
+  uint64_t n = 0, N = 0;
+  std::vector<felt> pub;
+  AirDesc air;
+  // CE cosets: CE coset u lives in LDE coset u << cstep; this rank evaluates [u0, u0 + cel)
+  uint32_t ce = 0, C = 0, logce = 0, cstep = 0, u0 = 0, cel = 0, celmax = 0;
+  felt g{};
+  zkp_transcript T;
+  Coin coin;
+  // device transcript and domain tables
+  uint32_t ncoef = 0;
+  uint32_t* dt_seed = nullptr;
+  felt *dt_cc = nullptr, *dt_zz = nullptr, *dt_pw = nullptr, *dt_aval = nullptr;
+  const felt* Sj0 = nullptr;
+  felt* cx = nullptr;
+  const felt* twn = nullptr;
+  // trace, composition, OOD, DEEP
+  const felt* d_trace = nullptr;
+  felt *coef = nullptr, *tlde = nullptr, *comp = nullptr, *acoef = nullptr, *clde = nullptr;
+  TreeShard ttree, ctree;
+  const uint32_t *troot_d = nullptr, *croot_d = nullptr;
+  felt wn_root{};
+  felt *deep_binv = nullptr, *dv = nullptr, *dgam = nullptr, *dk = nullptr, *deep = nullptr;
+  PointMap deep_pm{};
+  std::vector<felt> ood_trace, ood_comp;  // filled by the host replay of the FRI round trip
+  // FRI, grinding, queries
+  uint32_t L = 0;
+  std::vector<FriLayer> layers;
+  std::vector<felt> remainder;
+  bool dev_tail = false;   // remainder + first grinding chunk on the device
+  bool dev_query = false;  // ... and the whole query tail (world 1)
+  FullGatherArgs ga{};
+  uint64_t* dpos = nullptr;
+  const uint32_t* full_d = nullptr;
+  std::vector<uint32_t> full_h;
+  std::vector<uint64_t> raw_pos;
+  felt* rem_d = nullptr;
+  uint32_t* rcommit_d = nullptr;
+  unsigned long long* dres = nullptr;
+  unsigned long long dnonce = ~0ull;
+  static constexpr uint64_t grind_chunk = 1ull << 22;
+  uint64_t nonce = 0;
+
+  ProofRun(zkp_ctx* c, zkp_comm* m, const zkp_proof_options* opts)
+      : ctx(c), cm(m), o(opts), st(c->stream), pf(c->prof) {
+    memset(&T, 0, sizeof T);
+  }
+  uint32_t ce_owner(uint32_t u) const { return (u << cstep) / Bl; }
+  uint32_t ce_first(uint32_t s) const {
+    uint32_t u = 0;
+    while (u < ce && ce_owner(u) < s) u++;
+    return u;
+  }
+  int init(int air_id, const felt* d_trace_in, uint32_t width, uint64_t n_rows, const zkp_felt* pub_elems,
+           uint64_t n_pub, uint8_t** proof, uint64_t* proof_len);
+  void setup();
+  void trace_stage(const zkp_felt* h_trace);
+  void constraint_stage();
+  void ood_stage();
+  void deep_stage();
+  void fri_stage();
+  FriCursor fri_layers();
+  void fri_round_trip(const FriCursor& c);
+  void grind_stage();
+  int finish(uint8_t** proof, uint64_t* proof_len, zkp_transcript* tr_out);
+};
+
+// option / shape checks and the derived shapes (ZKP_ERR_* on a bad request)
+int ProofRun::init(int air_id, const felt* d_trace_in, uint32_t width, uint64_t n_rows, const zkp_felt* pub_elems,
+                   uint64_t n_pub, uint8_t** proof, uint64_t* proof_len) {
+  d_trace = d_trace_in;
+  w = width;
+  n = n_rows;
   int rc = check_options(o);
   if (rc) return rc;
   if (n < 8 || (n & (n - 1)) || w == 0 || w > 255) return ZKP_ERR_TRACE_SHAPE;
   if (!proof || !proof_len || (n_pub && !pub_elems)) return ZKP_ERR_ARGUMENT;
-  const uint32_t B = o->blowup_factor, F = o->fri_folding_factor;
-  const uint32_t logn = ilog2(n), logB = ilog2(B), logN = logn + logB;
-  const uint64_t N = 1ull << logN;
+  B = o->blowup_factor; F = o->fri_folding_factor;
+  logn = ilog2(n); logB = ilog2(B); logN = logn + logB;
+  N = 1ull << logN;
   if (logN > 32) return ZKP_ERR_TRACE_SHAPE;
   // coset sharding: rank r owns the LDE cosets [j0, j0 + Bl)
-  const uint32_t R = (uint32_t)cm->world, rank = (uint32_t)cm->rank;
+  R = (uint32_t)cm->world; rank = (uint32_t)cm->rank;
   if (R == 0 || (R & (R - 1)) || R > B || rank >= R) return ZKP_ERR_ARGUMENT;
-  const uint32_t logR = ilog2(R), Bl = B >> logR, logBl = logB - logR, j0 = rank * Bl;
+  logR = ilog2(R); Bl = B >> logR; logBl = logB - logR; j0 = rank * Bl;
   if (R > 1 && logn < logR + 8) return ZKP_ERR_TRACE_SHAPE;  // each rank's Merkle range needs >= 256 rows/coset
-  std::vector<felt> pub(n_pub);
+  pub.resize(n_pub);
   for (uint64_t i = 0; i < n_pub; i++) pub[i] = make(pub_elems[i].lo, pub_elems[i].hi);
-  AirDesc air;
   rc = build_air(air, air_id, w, n, pub);
   if (rc) return rc;
-  const uint32_t ce = air.ce_blowup(), C = air.comp_cols();
+  ce = air.ce_blowup(); C = air.comp_cols();
   if (B < ce) return ZKP_ERR_INVALID_OPTIONS;
-  const uint32_t logce = ilog2(ce);
+  logce = ilog2(ce);
   if (ce > 16 || C > ce) return ZKP_ERR_UNSUPPORTED_AIR;
   // CE coset u lives in LDE coset u << (logB - logce); this rank evaluates the CE cosets it holds
-  const uint32_t cstep = logB - logce;
-  auto ce_owner = [&](uint32_t u) { return (u << cstep) / Bl; };
-  auto ce_first = [&](uint32_t s) { uint32_t u = 0; while (u < ce && ce_owner(u) < s) u++; return u; };
-  const uint32_t u0 = ce_first(rank);
-  uint32_t cel = 0;
+  cstep = logB - logce;
+  u0 = ce_first(rank);
+  cel = 0;
   while (u0 + cel < ce && ce_owner(u0 + cel) == rank) cel++;
-  const uint32_t celmax = ce >= R ? ce / R : 1;
-  const felt g = felt_u64(3);
-  zkp_transcript T;
-  memset(&T, 0, sizeof T);
-  hipStream_t st = ctx->stream;
-  Prof& pf = ctx->prof;
+  celmax = ce >= R ? ce / R : 1;
+  g = felt_u64(3);
+  ood_trace.assign(2 * (size_t)w, felt{});
+  ood_comp.assign(C, felt{});
+  return 0;
+}
 
+// 1. channel: Context::to_elements || pub_inputs.to_elements; device transcript seed, domain tables
+void ProofRun::setup() {
   ctx->sync();
   ctx->ring_reset();
   ctx->stage_begin();
   // 1. channel: Context::to_elements || pub_inputs.to_elements
-  Coin coin;
   {
     std::vector<felt> se = context_elements(air, o);
     se.insert(se.end(), pub.begin(), pub.end());
@@ -1033,12 +1120,12 @@ int prove_impl(zkp_ctx* ctx, zkp_comm* cm, int air_id, const felt* d_trace, uint
   // device transcript: the coin state lives in HBM from here until
   // the OOD download; the device draws the composition coefficients and z, the
   // host replays both draws from the downloaded roots and checks them
-  const uint32_t ncoef = air.num_t + (uint32_t)air.a_col.size();
-  uint32_t* dt_seed = ctx->buf<uint32_t>("dt_seed", 8);
-  felt* dt_cc = ctx->buf<felt>("dt_cc", ncoef);
-  felt* dt_zz = ctx->buf<felt>("dt_zz", 2);
-  felt* dt_pw = ctx->buf<felt>("dt_pw", 2 * (size_t)logn);
-  felt* dt_aval = ctx->buf<felt>("dt_aval", air.a_val.size());
+  ncoef = air.num_t + (uint32_t)air.a_col.size();
+  dt_seed = ctx->buf<uint32_t>("dt_seed", 8);
+  dt_cc = ctx->buf<felt>("dt_cc", ncoef);
+  dt_zz = ctx->buf<felt>("dt_zz", 2);
+  dt_pw = ctx->buf<felt>("dt_pw", 2 * (size_t)logn);
+  dt_aval = ctx->buf<felt>("dt_aval", air.a_val.size());
   {
     uint32_t sw[8];
     for (int i = 0; i < 8; i++)
@@ -1048,19 +1135,21 @@ int prove_impl(zkp_ctx* ctx, zkp_comm* cm, int air_id, const felt* d_trace, uint
     ctx->upload(dt_aval, air.a_val.data(), air.a_val.size() * 16);
   }
   ctx->ensure_coset(logn, logB, logce);
-  const felt* Sj0 = ctx->S(logn, logB) + (uint64_t)j0 * n;
+  Sj0 = ctx->S(logn, logB) + (uint64_t)j0 * n;
   // domain points: coset offsets g*w_N^j (LDE cosets) and g*w_M^u (CE cosets), w_n^t table
   // (domain-only: cached per (n, B, ce), so no upload sits between the proof's kernels)
-  felt* cx = coset_points(ctx, logn, logB, logce);
-  const felt* twn = ctx->tws(logN) + ((1ull << (logn - 1)) - 1);
+  cx = coset_points(ctx, logn, logB, logce);
+  twn = ctx->tws(logN) + ((1ull << (logn - 1)) - 1);
   ctx->stage_end("0_setup");
+}
 
+// 2. trace LDE + commitment (DefaultTraceLde::new)
+void ProofRun::trace_stage(const zkp_felt* h_trace) {
   // 2. trace LDE + commitment (DefaultTraceLde::new): interpolation (by column
   // over the ranks for wide traces), coset LDE of this rank's cosets, sharded
   // row commitment
-  felt* coef = ctx->buf<felt>("coef", (size_t)(w + C) * n);
-  felt* tlde = ctx->buf<felt>("tlde", (size_t)w * Bl * n);
-  TreeShard ttree;
+  coef = ctx->buf<felt>("coef", (size_t)(w + C) * n);
+  tlde = ctx->buf<felt>("tlde", (size_t)w * Bl * n);
   bool coeffs_drawn = false;
   // wide traces shard the interpolation by column (cpt columns per rank) when the
   // width divides over the ranks; narrow ones interpolate on every rank
@@ -1155,22 +1244,26 @@ int prove_impl(zkp_ctx* ctx, zkp_comm* cm, int air_id, const felt* d_trace, uint
     coeffs_drawn = commit_rows(ctx, cm, 0, tlde, n, w, logB, logn, R > 1, "ttree", ttree, T.trace_root,
                                /*fetch_root=*/false, &draw);
   }
-  const uint32_t* troot_d = R > 1 ? ttree.top_d + 8 : ttree.nodes + 8;  // sharded: the device-built top
-  ctx->stage_end("1_trace_commit");
-
-  // 3. constraint composition coefficients (drawn on the device) + evaluation (DefaultConstraintEvaluator)
+  troot_d = R > 1 ? ttree.top_d + 8 : ttree.nodes + 8;  // sharded: the device-built top
+  // the composition coefficients (drawn on the device from the trace root)
   if (!coeffs_drawn) launch_dt_draw_coeffs(pf, st, dt_seed, troot_d, o->batching_constraints, ncoef, dt_cc);
-  felt* comp = ctx->buf<felt>("comp", (size_t)(cel ? cel : 1) * n);
+  ctx->stage_end("1_trace_commit");
+}
+
+// 3-4. constraint evaluation (DefaultConstraintEvaluator) and the composition
+// polynomial + its commitment (CompositionPoly::new + DefaultConstraintCommitment)
+void ProofRun::constraint_stage() {
+  // 3. constraint evaluation (DefaultConstraintEvaluator) with the device-drawn coefficients
+  comp = ctx->buf<felt>("comp", (size_t)(cel ? cel : 1) * n);
   constraint_eval(ctx, air, logn, logB, logce, u0, cel, j0, logBl, cx, twn, dt_cc, dt_aval, tlde, comp, coef, cm);
 
   // 4. composition polynomial + commitment (CompositionPoly::new +
   // DefaultConstraintCommitment): per-CE-coset interpolation, exchange of
   // coefficient slices, ce-point DFT per coefficient, all-gather, coset LDE
-  felt* acoef = coef + (size_t)w * n;
-  felt* clde = ctx->buf<felt>("clde", (size_t)C * Bl * n);
-  TreeShard ctree;
+  acoef = coef + (size_t)w * n;
+  clde = ctx->buf<felt>("clde", (size_t)C * Bl * n);
   bool z_drawn = false;
-  const felt wn_root = root_of_unity(logn);
+  wn_root = root_of_unity(logn);
   {
     // this rank's slice of bit-reversed coefficient positions: [p0, p0 + nR)
     const uint64_t nR = n >> logR, p0 = (uint64_t)rank * nR;
@@ -1236,30 +1329,36 @@ int prove_impl(zkp_ctx* ctx, zkp_comm* cm, int air_id, const felt* d_trace, uint
     z_drawn = commit_rows(ctx, cm, 0, clde, n, C, logB, logn, R > 1, "ctree", ctree, T.constraint_root,
                           /*fetch_root=*/false, &draw);
   }
-  const uint32_t* croot_d = R > 1 ? ctree.top_d + 8 : ctree.nodes + 8;
+  croot_d = R > 1 ? ctree.top_d + 8 : ctree.nodes + 8;
   if (!z_drawn) launch_dt_draw_z(pf, st, dt_seed, croot_d, wn_root, logn, dt_zz, dt_pw);
   ctx->stage_end("2_constraints_commit");
+}
 
+// 5. OOD frame and the DEEP coefficients (device transcript)
+void ProofRun::ood_stage() {
   // 5. OOD frame (sharded: every rank holds all coefficients and sums 1/R of each array's blocks)
   // the DEEP denominators (x - z)(x - zg) only need z: their batch-inversion
   // phases run on the side stream beside the OOD evaluation and its transcript
-  felt* deep_binv = ctx->buf<felt>("binv", ((uint64_t)Bl * n) / 2048 + 1);
-  const PointMap deep_pm{cx + j0, twn, logn};
+  deep_binv = ctx->buf<felt>("binv", ((uint64_t)Bl * n) / 2048 + 1);
+  deep_pm = PointMap{cx + j0, twn, logn};
   HIP_CHECK(hipEventRecord(ctx->ev_fork, st));
   HIP_CHECK(hipStreamWaitEvent(ctx->side, ctx->ev_fork, 0));
   launch_deep_denominators(pf, ctx->side, deep_pm, (uint64_t)Bl * n, dt_zz, dt_pw, deep_binv);
   HIP_CHECK(hipEventRecord(ctx->ev_join, ctx->side));
   // OOD frame and DEEP coefficients on the device (device transcript); the host
   // replays both at the FRI round trip
-  felt* dv = ood_launch(ctx, coef, w + C, w, logn, dt_pw, cm);  // composition columns at z only
-  felt* dgam = ctx->buf<felt>("gamma", w + C);
-  felt* dk = ctx->buf<felt>("dt_dk", 4);
+  dv = ood_launch(ctx, coef, w + C, w, logn, dt_pw, cm);  // composition columns at z only
+  dgam = ctx->buf<felt>("gamma", w + C);
+  dk = ctx->buf<felt>("dt_dk", 4);
   HIP_CHECK(hipMemcpyAsync(dk, dt_zz, 32, hipMemcpyDeviceToDevice, st));
   launch_dt_deep_coeffs(pf, st, dt_seed, dv, w, C, o->batching_deep, dgam, dk);
   ctx->stage_end("3_ood");
+}
 
+// 6. DEEP composition evaluations over this rank's cosets
+void ProofRun::deep_stage() {
   // 6. DEEP composition evaluations over this rank's cosets (coset-major)
-  felt* deep = ctx->buf<felt>("deep", (size_t)Bl * n);
+  deep = ctx->buf<felt>("deep", (size_t)Bl * n);
   {
     DeepArgs da;
     da.w = w; da.C = C; da.logB = logB; da.logn = logn; da.logN = logN;
@@ -1271,31 +1370,29 @@ int prove_impl(zkp_ctx* ctx, zkp_comm* cm, int air_id, const felt* d_trace, uint
     deep_evaluations(ctx, cm, st, da, coef, n, Sj0, logN, deep);
   }
   ctx->stage_end("4_deep_launch");
+}
 
-  std::vector<felt> ood_trace(2 * (size_t)w), ood_comp(C);  // filled by the host replay below
+// 7. FRI layers (FriProver::build_layers), remainder, the proof's host round trip
+// and the host replay of the device transcript
+void ProofRun::fri_stage() {
+  const FriCursor c = fri_layers();
+  fri_round_trip(c);
+  ctx->stage_end("5_fri");
+}
 
+// the layer loop on the device: trees, coin steps, folds; then the remainder,
+// the first grinding chunk and (world 1) the query tail
+FriCursor ProofRun::fri_layers() {
   // 7. FRI layers (FriProver::build_layers), folding factor 16. Layers stay
   // coset-sharded while each rank's Merkle range has >= 16 rows per coset,
   // then are all-gathered and finished identically on every rank.
-  uint32_t L = 0;
+  L = 0;
   {
     uint64_t D = N, maxrem = (uint64_t)(o->fri_remainder_max_degree + 1) * B;
     while (D > maxrem) { D /= F; L++; }
   }
-  std::vector<FriLayer> layers(L + 1);
-  std::vector<felt> remainder;
-  bool dev_tail = false;  // remainder + first grinding chunk on the device
-  bool dev_query = false;  // ... and the whole query tail (world 1)
-  FullGatherArgs ga{};
-  uint64_t* dpos = nullptr;
-  const uint32_t* full_d = nullptr;
-  std::vector<uint32_t> full_h;
-  std::vector<uint64_t> raw_pos;
-  felt* rem_d = nullptr;
-  uint32_t* rcommit_d = nullptr;
-  unsigned long long* dres = ctx->buf<unsigned long long>("grind_res", 1);
-  unsigned long long dnonce = ~0ull;
-  const uint64_t grind_chunk = 1ull << 22;
+  layers.assign(L + 1, FriLayer{});
+  dres = ctx->buf<unsigned long long>("grind_res", 1);
   {
     uint64_t tot_e = 0, D = N;
     for (uint32_t l = 0; l < L; l++) { tot_e += D / F; D /= F; }
@@ -1435,6 +1532,19 @@ int prove_impl(zkp_ctx* ctx, zkp_comm* cm, int air_id, const felt* d_trace, uint
       raw_pos.resize(o->num_queries);
       full_d = dfull;
     }
+    return FriCursor{E, m, D, off, coin_d, alphas_d, roots_d};
+  }
+}
+
+// the proof's host round trip and the replay of the device transcript
+void ProofRun::fri_round_trip(const FriCursor& c) {
+  felt* const E = c.E;
+  const uint64_t m = c.m, D = c.D;
+  const felt off = c.off;
+  uint32_t* const coin_d = c.coin_d;
+  felt* const alphas_d = c.alphas_d;
+  uint32_t* const roots_d = c.roots_d;
+  {
     // the proof's first host round trip: the device transcript so far (commitment
     // roots, coefficients, z, OOD frame, DEEP coefficients, FRI roots + alphas)
     // and the last FRI layer
@@ -1517,10 +1627,10 @@ int prove_impl(zkp_ctx* ctx, zkp_comm* cm, int air_id, const felt* d_trace, uint
     }
     T.num_fri_layers = L;
   }
-  ctx->stage_end("5_fri");
+}
 
-  // 8. grinding: minimum nonce >= 1 (every rank finds the same nonce)
-  uint64_t nonce = 0;
+void ProofRun::grind_stage() {
+  nonce = 0;
   if (o->grinding_factor == 0) {
     nonce = 1;
   } else {
@@ -1549,7 +1659,10 @@ int prove_impl(zkp_ctx* ctx, zkp_comm* cm, int air_id, const felt* d_trace, uint
   }
   T.pow_nonce = nonce;
   ctx->stage_end("6_grind");
+}
 
+// 9-10. query positions, openings, serialization (≙ Proof::to_bytes)
+int ProofRun::finish(uint8_t** proof, uint64_t* proof_len, zkp_transcript* tr_out) {
   // 9. query positions
   std::vector<uint64_t> pos = coin.draw_integers(o->num_queries, N, nonce);
   if (dev_query && pos != raw_pos) throw ZkpFail{ZKP_ERR_DEVICE, "device query positions diverged from the host"};
@@ -1600,6 +1713,25 @@ int prove_impl(zkp_ctx* ctx, zkp_comm* cm, int air_id, const felt* d_trace, uint
   *proof_len = wr.b.size();
   if (tr_out) *tr_out = T;
   return 0;
+}
+
+// h_trace (nullable): the trace is still in host memory and d_trace is its
+// device buffer; the upload is pipelined with the trace interpolation and LDE
+// by column groups (wide traces), so PCIe overlaps the first stage's kernels.
+int prove_impl(zkp_ctx* ctx, zkp_comm* cm, int air_id, const felt* d_trace, uint32_t w, uint64_t n,
+               const zkp_felt* pub_elems, uint64_t n_pub, const zkp_proof_options* o, uint8_t** proof,
+               uint64_t* proof_len, zkp_transcript* tr_out, const zkp_felt* h_trace = nullptr) {
+  ProofRun run(ctx, cm, o);
+  int rc = run.init(air_id, d_trace, w, n, pub_elems, n_pub, proof, proof_len);
+  if (rc) return rc;
+  run.setup();
+  run.trace_stage(h_trace);
+  run.constraint_stage();
+  run.ood_stage();
+  run.deep_stage();
+  run.fri_stage();
+  run.grind_stage();
+  return run.finish(proof, proof_len, tr_out);
 }
 
 template <typename F>
