@@ -1,0 +1,14 @@
+#!/bin/bash
+# Round-end measurement, part 1: C2 and C3 bench lines, the C2 timeline, the C2 rocprofv3 profile.
+set -o pipefail
+mkdir -p gpurun_out
+timeout -k 10 240 python bench.py --steps 20 --stats > gpurun_out/b_c2.json 2> gpurun_out/b_c2.err || { tail -20 gpurun_out/b_c2.err; exit 1; }
+timeout -k 10 240 python bench.py --air agg --steps 10 --no-cpu-baseline --stats > gpurun_out/b_c3.json 2> gpurun_out/b_c3.err || { tail -20 gpurun_out/b_c3.err; exit 1; }
+timeout -k 10 120 python3 scripts/timeline.py > gpurun_out/timeline_r03.txt 2>&1 || { tail -5 gpurun_out/timeline_r03.txt; exit 1; }
+bash scripts/profile_round.sh r03 || exit 1
+python3 -c "
+import json
+for f in ['b_c2','b_c3']:
+    d=json.loads(open('gpurun_out/'+f+'.json').read().strip().splitlines()[-1])
+    print(f, d['value'], d['ms_per_step'], d['device_resident_ms'], d['roofline']['frac'], d['roofline']['avg_launch_ms'], d['launches']['per_proof'])
+"

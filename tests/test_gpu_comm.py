@@ -74,3 +74,24 @@ def test_local_group_check_then_prove(ctx):
     single, _ = ctx.prove(AIR_MIMC, trace.data, pub, opts)
     res = prove_local_group(2, AIR_MIMC, trace.data, pub, opts)
     assert all(b == single for b, _ in res)
+
+
+def test_comm_check_detects_a_corrupting_transport(ctx):
+    """A caller transport that flips one byte of an all-gather block must make the
+    check fail (naming the peer and word), not pass silently."""
+    import ctypes
+
+    def a2a(send, recv, block):
+        ctypes.memmove(recv, send, block)  # world 1: block 0 to itself
+
+    def ag(send, recv, nbytes):
+        ctypes.memmove(recv, send, nbytes)
+        b = (ctypes.c_uint8 * nbytes).from_address(recv)
+        b[nbytes // 2] ^= 0x40
+
+    comm = _native.host_comm(0, 1, a2a, ag)
+    try:
+        with pytest.raises(_native.ZkpError, match="all_gather"):
+            ctx.comm_check(comm, 1 << 16)
+    finally:
+        comm.close()

@@ -1404,9 +1404,11 @@ void launch_merkle_from_shards(Prof& prof, hipStream_t s, const uint32_t* recv, 
 
 // top levels of a sharded tree from the all-gathered subtree roots (R <= 64):
 // top[R + s] = root of rank s's subtree, top[k] = merge(top[2k], top[2k+1]);
-// the root (top[1]) stays on the device for the coin kernels
-__global__ __launch_bounds__(64) void k_shard_top(const uint32_t* __restrict__ roots, uint32_t R,
-                                                  uint32_t* __restrict__ top) {
+// the root (top[1]) stays on the device, and the block then runs the
+// commitment's coin step (MerkleTail op: coefficients, z or the FRI alpha) as a
+// world-1 tree's last block does
+__global__ __launch_bounds__(256) void k_shard_top(const uint32_t* __restrict__ roots, uint32_t R,
+                                                   uint32_t* __restrict__ top, MerkleTail tail) {
   const uint32_t t = threadIdx.x;
   if (t < R)
     for (int i = 0; i < 8; i++) top[(R + t) * 8 + i] = roots[t * 8 + i];
@@ -1420,10 +1422,15 @@ __global__ __launch_bounds__(64) void k_shard_top(const uint32_t* __restrict__ r
       store_digest(top + (h + t) * 8, o);
     }
   }
+  __syncthreads();
+  if (tail.op != MERKLE_TAIL_NONE) merkle_tail_op(tail, top + 8);  // whole block
 }
 
-void launch_shard_top(Prof& prof, hipStream_t s, const uint32_t* roots, uint32_t R, uint32_t* top) {
-  LAUNCH(prof, "merkle_top9", s, (double)R * 64.0, hipLaunchKernelGGL(k_shard_top, dim3(1), dim3(64), 0, s, roots, R, top));
+void launch_shard_top(Prof& prof, hipStream_t s, const uint32_t* roots, uint32_t R, uint32_t* top,
+                      const MerkleTail* tail) {
+  const MerkleTail tl = tail ? *tail : MerkleTail{};
+  LAUNCH(prof, "merkle_top9", s, (double)R * 64.0,
+         hipLaunchKernelGGL(k_shard_top, dim3(1), dim3(256), 0, s, roots, R, top, tl));
 }
 
 void launch_dt_draw_coeffs(Prof& prof, hipStream_t s, uint32_t* seed, const uint32_t* root, uint32_t method,

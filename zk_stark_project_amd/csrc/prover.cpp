@@ -334,8 +334,9 @@ struct TreeShard {
 // mode 0 = LDE rows (cols columns, n rows per coset), mode 1 = FRI rows (16
 // values, 2^logrows rows per coset). Unsharded sources hold all B cosets.
 // Unsharded trees finish in the last block of their top launch (MerkleTail);
-// with coin (FRI layers) that block also runs the layer's coin step, and the
-// function returns true when it did.
+// sharded trees in k_shard_top over the all-gathered subtree roots. With coin
+// (coefficients, z or a FRI layer's alpha) that block also runs the coin step,
+// and the function returns true when it did.
 bool commit_rows(zkp_ctx* ctx, zkp_comm* cm, int mode, const felt* src, uint64_t n, uint32_t cols, uint32_t logB,
                  uint32_t logrows, bool sharded, const std::string& name, TreeShard& tr, uint8_t root[32],
                  bool fetch_root = true, const MerkleTail* coin = nullptr) {
@@ -390,13 +391,13 @@ bool commit_rows(zkp_ctx* ctx, zkp_comm* cm, int mode, const felt* src, uint64_t
   uint32_t* roots = ctx->buf<uint32_t>("shard_roots", (size_t)8 * R);
   cm->all_gather(st, tr.nodes + 8, roots, 32);
   tr.top_d = ctx->buf<uint32_t>(name + "_top", (size_t)16 * R);
-  launch_shard_top(pf, st, roots, R, tr.top_d);
+  launch_shard_top(pf, st, roots, R, tr.top_d, coin);  // + the coin step, as a world-1 tree's last block
   tr.top.assign(2 * R, {});
   if (fetch_root) {
     ctx->download(tr.top.data(), tr.top_d, (size_t)64 * R);
     memcpy(root, tr.top[1].data(), 32);
   }
-  return false;
+  return coin && coin->op != MERKLE_TAIL_NONE;
 }
 
 // evaluate bit-reversed coefficient arrays (scaled by n) at x0, x1 -> values (x n^-1)

@@ -100,8 +100,10 @@ bool merkle_upper(Prof& prof, hipStream_t s, uint32_t* nodes, uint64_t L, const 
 void launch_leaf_hash_shard(Prof& prof, hipStream_t s, int mode, const felt* src, uint64_t n, uint32_t cols,
                             uint32_t logBl, uint32_t logrows, uint32_t logrr, uint32_t logK, uint32_t k,
                             uint32_t* send);
-// sharded tree tops (R <= 64 subtree roots, all-gathered) -> top[1..2R) on the device
-void launch_shard_top(Prof& prof, hipStream_t s, const uint32_t* roots, uint32_t R, uint32_t* top);
+// sharded tree tops (R <= 64 subtree roots, all-gathered) -> top[1..2R) on the device,
+// then the tail's coin step on the root (tail nullable / MERKLE_TAIL_NONE: none)
+void launch_shard_top(Prof& prof, hipStream_t s, const uint32_t* roots, uint32_t R, uint32_t* top,
+                      const MerkleTail* tail);
 void launch_merkle_from_shards(Prof& prof, hipStream_t s, const uint32_t* recv, uint32_t logB, uint32_t logrr,
                                uint32_t logK, uint32_t* nodes);
 // internal nodes nodes[1..L) from leaves nodes[L..2L)
