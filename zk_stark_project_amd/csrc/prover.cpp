@@ -1207,19 +1207,35 @@ void ProofRun::trace_stage(const zkp_felt* h_trace) {
       }
       h_trace = nullptr;  // resident on every rank from here
     }
-    // column groups: one for device-resident traces; host traces upload group g+1
-    // on the copy stream while the main stream interpolates and extends group g
-    const uint32_t groups = h_trace ? (w >= 16 ? 8u : (w >= 4 ? 4u : 1u)) : 1u;
-    const uint32_t cg = (w + groups - 1) / groups;
-    if (groups > 1) ctx->events(groups);
-    if (h_trace && groups > 1) {  // the copy stream starts after everything already queued
+    // column groups: one for device-resident traces. Host traces upload group g+1
+    // on the copy stream while the main stream interpolates and extends group g;
+    // the groups grow geometrically (x1.5 from ~w/40 columns: C3 3, 4, 6, ..., 38),
+    // so only the small first group's upload is exposed and every later one hides
+    // behind the previous group's LDE (a column's upload takes ~0.55x its LDE at C3)
+    std::vector<std::pair<uint32_t, uint32_t>> grp;  // (first column, columns)
+    static const uint32_t growth =  // percent (A/B switch ZKP_UPLOAD_GROWTH)
+        getenv("ZKP_UPLOAD_GROWTH") ? std::max(110, atoi(getenv("ZKP_UPLOAD_GROWTH"))) : 150u;
+    if (h_trace && w >= 4) {
+      uint32_t cw = std::max(1u, w / 40);
+      for (uint32_t c = 0; c < w;) {
+        cw = std::min(cw, w - c);
+        grp.push_back({c, cw});
+        c += cw;
+        cw = std::max(cw + 1, cw * growth / 100);
+      }
+    } else {
+      grp.push_back({0u, w});
+    }
+    const bool piped = h_trace && grp.size() > 1;
+    if (piped) {  // the copy stream starts after everything already queued
+      ctx->events(grp.size());
       HIP_CHECK(hipEventRecord(ctx->ev_fork, st));
       HIP_CHECK(hipStreamWaitEvent(ctx->side, ctx->ev_fork, 0));
     }
-    for (uint32_t c0 = 0, g = 0; c0 < w; c0 += cg, g++) {
-      const uint32_t cw = c0 + cg <= w ? cg : w - c0;
+    for (uint32_t g = 0; g < grp.size(); g++) {
+      const uint32_t c0 = grp[g].first, cw = grp[g].second;
       felt* dcol = const_cast<felt*>(d_trace) + (size_t)c0 * n;
-      if (h_trace && groups > 1) {
+      if (piped) {
         HIP_CHECK(hipMemcpyAsync(dcol, h_trace + (size_t)c0 * n, (size_t)cw * n * 16, hipMemcpyHostToDevice,
                                  ctx->side));
         HIP_CHECK(hipEventRecord(ctx->up_ev[g], ctx->side));
