@@ -56,6 +56,9 @@ struct zkp_ctx {
   // side stream: work that only needs domain data runs there while the main
   // stream waits on a host round trip (ordered back in with events)
   hipStream_t side = nullptr;
+  // copy stream: a sharded wide trace's column uploads and interpolations, ahead
+  // of the main stream's coset LDEs (ordered in with events)
+  hipStream_t copy = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   Prof prof;
   std::string err;
@@ -297,6 +300,7 @@ struct zkp_ctx {
     for (auto e : up_ev) (void)hipEventDestroy(e);
     if (ev_fork) (void)hipEventDestroy(ev_fork);
     if (ev_join) (void)hipEventDestroy(ev_join);
+    if (copy) (void)hipStreamDestroy(copy);
     if (side) (void)hipStreamDestroy(side);
     if (stream) (void)hipStreamDestroy(stream);
   }
@@ -1167,18 +1171,22 @@ void ProofRun::trace_stage(const zkp_felt* h_trace) {
     while (cpt % K) K--;
     const uint32_t cpr = cpt / K;
     felt* own = ctx->buf<felt>("coef_own", (size_t)cpt * n);
-    ctx->events(2 * (size_t)K);
+    ctx->events(3 * (size_t)K);
+    // the copy stream starts after everything already queued on the main stream
+    HIP_CHECK(hipEventRecord(ctx->ev_fork, st));
+    HIP_CHECK(hipStreamWaitEvent(ctx->copy, ctx->ev_fork, 0));
+    HIP_CHECK(hipStreamWaitEvent(ctx->side, ctx->ev_fork, 0));
+    // per round k: upload (host traces) + interpolation on the copy stream, the
+    // coefficient all-gather on the side stream, the coset LDE on the main stream;
+    // a pageable upload holds the host, and by then round k-1's LDE is queued
     for (uint32_t k = 0; k < K; k++) {
-      const uint64_t cown = (uint64_t)k * R * cpr + (uint64_t)rank * cpr;
+      const uint64_t cown = (uint64_t)k * R * cpr + (uint64_t)rank * cpr, c0 = (uint64_t)k * R * cpr;
       felt* dcol = const_cast<felt*>(d_trace) + cown * n;
       if (h_trace)
-        HIP_CHECK(hipMemcpyAsync(dcol, h_trace + cown * n, (size_t)cpr * n * 16, hipMemcpyHostToDevice, st));
+        HIP_CHECK(hipMemcpyAsync(dcol, h_trace + cown * n, (size_t)cpr * n * 16, hipMemcpyHostToDevice, ctx->copy));
       NttBatch ib{dcol, own + (size_t)k * cpr * n, nullptr, n, n, 1, 1, cpr};
-      launch_ntt(pf, st, ib, logn, false, ctx->itws(logN), logN);
-      HIP_CHECK(hipEventRecord(ctx->up_ev[k], st));
-    }
-    for (uint32_t k = 0; k < K; k++) {
-      const uint64_t c0 = (uint64_t)k * R * cpr;
+      launch_ntt(pf, ctx->copy, ib, logn, false, ctx->itws(logN), logN);
+      HIP_CHECK(hipEventRecord(ctx->up_ev[k], ctx->copy));
       HIP_CHECK(hipStreamWaitEvent(ctx->side, ctx->up_ev[k], 0));
       cm->all_gather(ctx->side, own + (size_t)k * cpr * n, coef + c0 * n, (size_t)cpr * n * 16);
       HIP_CHECK(hipEventRecord(ctx->up_ev[K + k], ctx->side));
@@ -1186,6 +1194,9 @@ void ProofRun::trace_stage(const zkp_felt* h_trace) {
       NttBatch lb{coef + c0 * n, tlde + c0 * Bl * n, Sj0, n, n, Bl, Bl, R * cpr * Bl};
       launch_ntt(pf, st, lb, logn, true, ctx->tws(logN), logN);
     }
+    // nothing on the copy stream may outlive the stage (the next proof reuses its buffers)
+    HIP_CHECK(hipEventRecord(ctx->up_ev[2 * K], ctx->copy));
+    HIP_CHECK(hipStreamWaitEvent(st, ctx->up_ev[2 * K], 0));
   } else {
     if (h_trace && R > 1) {
       // sharded host trace: each rank uploads only its 1/R row
@@ -1794,6 +1805,7 @@ int zkp_ctx_create(int device, zkp_ctx** out) {
   c->device = device;
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&c->copy, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess) {
     delete c;
