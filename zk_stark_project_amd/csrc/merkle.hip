@@ -83,7 +83,18 @@ struct MerkleArgs {
   uint32_t* nodes;
   uint64_t L;       // leaves of this (sub)tree level
   MerkleTail tail;  // k_merkle_fused: finish the tree (+ FRI coin step) in the last block
+  LastCol lc;       // k_merkle_leaf2<COLS, true>: column COLS-1 derived from H (zkp_internal.hpp)
 };
+
+// v[COLS-1] = (h - sum_{c<COLS-1} kappa^c v[c]) * kappa^-(COLS-1)  (LastCol; Horner
+// over the known columns: COLS-1 products)
+template <int COLS>
+__device__ __forceinline__ felt derive_last(const felt* v, felt h, felt kappa, felt kinv) {
+  felt acc = v[COLS - 2];
+#pragma unroll
+  for (int c = COLS - 3; c >= 0; c--) acc = add(mul(acc, kappa), v[c]);
+  return mul(sub(h, acc), kinv);
+}
 
 template <int MODE>
 __device__ __forceinline__ void merkle_leaf(const MerkleArgs& a, uint64_t i, uint32_t d[8]) {
@@ -339,18 +350,31 @@ __device__ __forceinline__ void lane_subtree(const MerkleArgs& a, uint64_t base,
 // inside its hash and its digest stores may alias the LDE (no restrict), so
 // the second row's loads wait behind the first row's hash and stores; here the
 // HBM latency of both rows is exposed once per lane.
-template <int COLS>
+// DERIVE: column COLS-1 is not read but derived from the constraint evaluations
+// (a.lc) and written out before hashing.
+template <int COLS, bool DERIVE = false>
 __global__ __launch_bounds__(256) void k_merkle_leaf2(MerkleArgs a) {
   const uint64_t lane = blockIdx.x * (uint64_t)256 + threadIdx.x;
   if (lane >= (a.L >> 1)) return;
   const uint64_t cstride = a.n << a.logB, bmask = (1ull << a.logB) - 1;
-  felt v[2][COLS];
+  constexpr int RD = DERIVE ? COLS - 1 : COLS;  // columns read from the source
+  felt v[2][COLS], h[2];
 #pragma unroll
   for (int r = 0; r < 2; r++) {
     const uint64_t i = 2 * lane + r;
-    const felt* base = a.src + (i & bmask) * a.n + (i >> a.logB);
+    const uint64_t off = (i & bmask) * a.n + (i >> a.logB);
+    const felt* base = a.src + off;
 #pragma unroll
-    for (int c = 0; c < COLS; c++) v[r][c] = base[c * cstride];
+    for (int c = 0; c < RD; c++) v[r][c] = base[c * cstride];
+    if constexpr (DERIVE) h[r] = a.lc.H[off];
+  }
+  if constexpr (DERIVE) {
+#pragma unroll
+    for (int r = 0; r < 2; r++) {
+      const uint64_t i = 2 * lane + r, j = i & bmask;
+      v[r][COLS - 1] = derive_last<COLS>(v[r], h[r], a.lc.kap[2 * j], a.lc.kap[2 * j + 1]);
+      a.lc.out[j * a.n + (i >> a.logB)] = v[r][COLS - 1];
+    }
   }
   uint32_t d0[8], d1[8], m[8];
   b3::hash_felts_c<COLS>([&](int c) { return v[0][c]; }, d0);
@@ -378,10 +402,11 @@ __global__ __launch_bounds__(256) void k_merkle_lane(MerkleArgs a) {
 // send_k[((s*Bl + jl)*rc + tc)], rr = rows / R.
 // COLS > 0 (narrow LDE rows, MODE 0): the row's felts are loaded into registers
 // before hashing (compile-time row length, see k_merkle_leaf2)
-template <int MODE, int COLS = 0>
+template <int MODE, int COLS = 0, bool DERIVE = false>
 __global__ __launch_bounds__(TPB) void k_leaf_hash_shard(const felt* __restrict__ src, uint64_t n, uint32_t cols,
                                                          uint32_t logBl, uint32_t logrows, uint32_t logrr,
-                                                         uint32_t logK, uint32_t k, uint32_t* __restrict__ send) {
+                                                         uint32_t logK, uint32_t k, uint32_t* __restrict__ send,
+                                                         LastCol lc) {
   const uint64_t q = blockIdx.x * (uint64_t)TPB + threadIdx.x;
   const uint32_t logrc = logrr - logK, logrk = logrows - logK;  // rows per chunk: per destination, in all
   if (q >= (1ull << (logrk + logBl))) return;
@@ -394,8 +419,13 @@ __global__ __launch_bounds__(TPB) void k_leaf_hash_shard(const felt* __restrict_
     const felt* base = src + jl * n + t;
     const uint64_t cstride = n << logBl;
     felt v[COLS];
+    constexpr int RD = DERIVE ? COLS - 1 : COLS;
 #pragma unroll
-    for (int c = 0; c < COLS; c++) v[c] = base[c * cstride];
+    for (int c = 0; c < RD; c++) v[c] = base[c * cstride];
+    if constexpr (DERIVE) {  // LastCol over the rank's cosets (lc.kap offset to coset j0)
+      v[COLS - 1] = derive_last<COLS>(v, lc.H[jl * n + t], lc.kap[2 * jl], lc.kap[2 * jl + 1]);
+      lc.out[jl * n + t] = v[COLS - 1];
+    }
     b3::hash_felts_c<COLS>([&](int c) { return v[c]; }, d);
   } else if (MODE == 0) {  // LDE row t of coset jl: (c*Bl + jl)*n + t
     const felt* base = src + jl * n + t;
@@ -1102,7 +1132,7 @@ bool merkle_upper(Prof& prof, hipStream_t s, uint32_t* nodes, uint64_t L, const 
 }
 
 bool launch_merkle_lde(Prof& prof, hipStream_t s, const felt* lde, uint32_t cols, uint32_t logB, uint64_t n,
-                       uint32_t* nodes, uint64_t L, const MerkleTail* tail) {
+                       uint32_t* nodes, uint64_t L, const MerkleTail* tail, const LastCol* lc) {
   MerkleArgs a{};
   a.src = lde;
   a.n = n;
@@ -1114,7 +1144,18 @@ bool launch_merkle_lde(Prof& prof, hipStream_t s, const felt* lde, uint32_t cols
   // lane subtrees, whose extra live digests cost waves (kbench_merkle.cpp)
   const uint32_t H = L >= 2 ? 1 : 0;
   static const bool no_preload = getenv("ZKP_NO_LEAF_PRELOAD") != nullptr;  // A/B switch
-  if (H == 1 && cols <= 8 && !no_preload) {
+  if (lc) {  // the caller checked merkle_can_derive(cols, L)
+    if (H != 1 || cols < 2 || cols > 8) abort();
+    a.lc = *lc;
+    const double bytes = (double)L * (cols * 16.0 + 48.0);
+    const dim3 g(blocks_for(L >> 1));
+#define ZKP_LEAF2D(CC)                                                                                      \
+  case CC:                                                                                                  \
+    LAUNCH(prof, "merkle_lde", s, bytes, hipLaunchKernelGGL((k_merkle_leaf2<CC, true>), g, dim3(256), 0, s, a)); \
+    break;
+    switch (cols) { ZKP_LEAF2D(2) ZKP_LEAF2D(3) ZKP_LEAF2D(4) ZKP_LEAF2D(5) ZKP_LEAF2D(6) ZKP_LEAF2D(7) ZKP_LEAF2D(8) }
+#undef ZKP_LEAF2D
+  } else if (H == 1 && cols <= 8 && !no_preload) {
     const double bytes = (double)L * (cols * 16.0 + 48.0);
     const dim3 g(blocks_for(L >> 1));
 #define ZKP_LEAF2(CC) \
@@ -1261,28 +1302,40 @@ void launch_fri_tail(Prof& prof, hipStream_t s, const FriTailArgs& a) {
 
 void launch_leaf_hash_shard(Prof& prof, hipStream_t s, int mode, const felt* src, uint64_t n, uint32_t cols,
                             uint32_t logBl, uint32_t logrows, uint32_t logrr, uint32_t logK, uint32_t k,
-                            uint32_t* send) {
+                            uint32_t* send, const LastCol* lc) {
   const uint64_t cnt = 1ull << (logrows - logK + logBl);
   const double bytes = (double)cnt * (cols * 16.0 + 32.0);
   const dim3 g(blocks_for(cnt));
+  const LastCol lcv = lc ? *lc : LastCol{};
 #define ZKP_SHARD_LEAF(CC)                                                                                   \
   case CC:                                                                                                   \
     LAUNCH(prof, "leaf_hash_shard", s, bytes,                                                                \
            hipLaunchKernelGGL((k_leaf_hash_shard<0, CC>), g, dim3(TPB), 0, s, src, n, cols, logBl, logrows, \
-                              logrr, logK, k, send));                                                        \
+                              logrr, logK, k, send, lcv));                                                   \
     break;
-  if (mode == 0 && cols <= 8) {
+#define ZKP_SHARD_LEAFD(CC)                                                                                  \
+  case CC:                                                                                                   \
+    LAUNCH(prof, "leaf_hash_shard", s, bytes,                                                                \
+           hipLaunchKernelGGL((k_leaf_hash_shard<0, CC, true>), g, dim3(TPB), 0, s, src, n, cols, logBl,    \
+                              logrows, logrr, logK, k, send, lcv));                                          \
+    break;
+  if (lc) {  // the caller checked merkle_can_derive
+    if (mode != 0 || cols < 2 || cols > 8) abort();
+    switch (cols) { ZKP_SHARD_LEAFD(2) ZKP_SHARD_LEAFD(3) ZKP_SHARD_LEAFD(4) ZKP_SHARD_LEAFD(5)
+                    ZKP_SHARD_LEAFD(6) ZKP_SHARD_LEAFD(7) ZKP_SHARD_LEAFD(8) }
+  } else if (mode == 0 && cols <= 8) {
     switch (cols) { ZKP_SHARD_LEAF(1) ZKP_SHARD_LEAF(2) ZKP_SHARD_LEAF(3) ZKP_SHARD_LEAF(4) ZKP_SHARD_LEAF(5)
                     ZKP_SHARD_LEAF(6) ZKP_SHARD_LEAF(7) ZKP_SHARD_LEAF(8) }
   } else if (mode == 0)
     LAUNCH(prof, "leaf_hash_shard", s, bytes,
            hipLaunchKernelGGL(k_leaf_hash_shard<0>, g, dim3(TPB), 0, s, src, n, cols, logBl,
-                              logrows, logrr, logK, k, send));
+                              logrows, logrr, logK, k, send, lcv));
   else
     LAUNCH(prof, "leaf_hash_shard", s, (double)cnt * (cols * 16.0 + 32.0),
            hipLaunchKernelGGL(k_leaf_hash_shard<1>, dim3(blocks_for(cnt)), dim3(TPB), 0, s, src, n, cols, logBl,
-                              logrows, logrr, logK, k, send));
+                              logrows, logrr, logK, k, send, lcv));
 }
+#undef ZKP_SHARD_LEAFD
 #undef ZKP_SHARD_LEAF
 
 void launch_merkle_from_shards(Prof& prof, hipStream_t s, const uint32_t* recv, uint32_t logB, uint32_t logrr,

@@ -343,7 +343,7 @@ struct TreeShard {
 // and the function returns true when it did.
 bool commit_rows(zkp_ctx* ctx, zkp_comm* cm, int mode, const felt* src, uint64_t n, uint32_t cols, uint32_t logB,
                  uint32_t logrows, bool sharded, const std::string& name, TreeShard& tr, uint8_t root[32],
-                 bool fetch_root = true, const MerkleTail* coin = nullptr) {
+                 bool fetch_root = true, const MerkleTail* coin = nullptr, const LastCol* lc = nullptr) {
   Prof& pf = ctx->prof;
   hipStream_t st = ctx->stream;
   const uint64_t L = 1ull << (logB + logrows);
@@ -355,7 +355,7 @@ bool commit_rows(zkp_ctx* ctx, zkp_comm* cm, int mode, const felt* src, uint64_t
     if (!ctx->have_cached("merkle_done")) HIP_CHECK(hipMemsetAsync(done, 0, 4, st));
     MerkleTail tail = coin ? *coin : MerkleTail{};
     tail.done = done;
-    bool ran = mode == 0 ? launch_merkle_lde(pf, st, src, cols, logB, n, tr.nodes, L, &tail)
+    bool ran = mode == 0 ? launch_merkle_lde(pf, st, src, cols, logB, n, tr.nodes, L, &tail, lc)
                          : launch_merkle_fri(pf, st, src, 1ull << logrows, logB, 16, tr.nodes, &tail);
     tr.top.assign(2, {});
     if (fetch_root) {  // otherwise the caller reads nodes[1] later
@@ -378,7 +378,7 @@ bool commit_rows(zkp_ctx* ctx, zkp_comm* cm, int mode, const felt* src, uint64_t
   const size_t chunk_words = (size_t)8 << (logBl + logrows - logK), block = (size_t)32 << (logBl + logrr - logK);
   ctx->events(K + 1);
   for (uint32_t k = 0; k < K; k++) {
-    launch_leaf_hash_shard(pf, st, mode, src, n, cols, logBl, logrows, logrr, logK, k, send + k * chunk_words);
+    launch_leaf_hash_shard(pf, st, mode, src, n, cols, logBl, logrows, logrr, logK, k, send + k * chunk_words, lc);
     HIP_CHECK(hipEventRecord(ctx->up_ev[k], st));
   }
   for (uint32_t k = 0; k < K; k++) {
@@ -622,6 +622,25 @@ void constraint_eval(zkp_ctx* ctx, const AirDesc& air, uint32_t logn, uint32_t l
     la.w_bstep1 = ec.w_last;
     linear(la, "binv_tu_" + dom);
   }
+}
+
+// LastCol constants per LDE coset j (ce == B): kappa_j = (g w_N^j)^n = g^n w_B^j and
+// kappa_j^-(C-1), at [2j, 2j+1] (shape-only: cached per (n, B, C))
+const felt* last_col_kappa(zkp_ctx* ctx, uint32_t logn, uint32_t logB, uint32_t C) {
+  const uint32_t B = 1u << logB;
+  const std::string key = "lastcol_kap_" + std::to_string(logn) + "_" + std::to_string(logB) + "_" +
+                          std::to_string(C);
+  felt* d = ctx->buf<felt>(key, 2 * (size_t)B);
+  if (!ctx->have_cached(key)) {
+    std::vector<felt> h(2 * (size_t)B);
+    const felt gn = pow_u64(felt_u64(3), 1ull << logn), wB = root_of_unity(logB);
+    for (uint32_t j = 0; j < B; j++) {
+      h[2 * j] = mul(gn, pow_u64(wB, j));
+      h[2 * j + 1] = inv(pow_u64(h[2 * j], C - 1));
+    }
+    ctx->upload(d, h.data(), h.size() * 16);
+  }
+  return d;
 }
 
 // constants of k_comp_dft: [g^-mn / ce for m < C | w_ce^-k for k < ce/2]
@@ -1295,17 +1314,22 @@ void ProofRun::constraint_stage() {
   {
     // this rank's slice of bit-reversed coefficient positions: [p0, p0 + nR)
     const uint64_t nR = n >> logR, p0 = (uint64_t)rank * nR;
+    // the last composition column derived in the leaf pass (LastCol): the rank's
+    // LDE cosets are exactly its CE cosets, whose evaluations stay in `comp`
+    static const bool no_derive = getenv("ZKP_NO_DERIVE_LAST") != nullptr;  // A/B switch
+    const bool derive = !no_derive && logce == logB && C >= 2 && C <= 8 && cel == Bl && u0 == j0;
+    felt* cint = derive ? ctx->buf<felt>("comp_int", (size_t)(cel ? cel : 1) * n) : comp;
     if (cel) {
-      NttBatch ib{comp, comp, nullptr, n, n, 1, 1, cel};
+      NttBatch ib{comp, cint, nullptr, n, n, 1, 1, cel};
       launch_ntt(pf, st, ib, logn, false, ctx->itws(logN), logN);
     }
-    felt* recv = comp;  // world 1: the rank holds every CE coset in full
+    felt* recv = cint;  // world 1: the rank holds every CE coset in full
     if (R > 1) {
       // send block s = positions [s*nR, (s+1)*nR) of every owned CE coset
       felt* send = ctx->buf<felt>("comp_send", (size_t)celmax * n);
       recv = ctx->buf<felt>("comp_recv", (size_t)celmax * n);
       for (uint32_t ul = 0; ul < cel; ul++)
-        HIP_CHECK(hipMemcpy2DAsync(send + (size_t)ul * nR, (size_t)celmax * nR * 16, comp + (size_t)ul * n, nR * 16,
+        HIP_CHECK(hipMemcpy2DAsync(send + (size_t)ul * nR, (size_t)celmax * nR * 16, cint + (size_t)ul * n, nR * 16,
                                    nR * 16, R, hipMemcpyDeviceToDevice, st));
       cm->all_to_all(st, send, recv, (size_t)celmax * nR * 16);
     }
@@ -1340,13 +1364,16 @@ void ProofRun::constraint_stage() {
         cm->all_gather(ctx->side, slice + (size_t)m * nR, acoef + (size_t)m * n, nR * 16);
         HIP_CHECK(hipEventRecord(ctx->up_ev[m], ctx->side));
         HIP_CHECK(hipStreamWaitEvent(st, ctx->up_ev[m], 0));
+        if (derive && m == C - 1) break;  // derived in the leaf pass (the OOD still reads its coefficients)
         NttBatch lb{acoef + (size_t)m * n, clde + (size_t)m * Bl * n, Sj0, n, n, Bl, Bl, Bl};
         launch_ntt(pf, st, lb, logn, true, ctx->tws(logN), logN);
       }
     } else {
-      NttBatch lb{acoef, clde, Sj0, n, n, Bl, Bl, C * Bl};
+      NttBatch lb{acoef, clde, Sj0, n, n, Bl, Bl, (derive ? C - 1 : C) * Bl};
       launch_ntt(pf, st, lb, logn, true, ctx->tws(logN), logN);
     }
+    LastCol lc{};
+    if (derive) lc = LastCol{comp, last_col_kappa(ctx, logn, logB, C) + 2 * (size_t)j0, clde + (size_t)(C - 1) * Bl * n};
     MerkleTail draw{};  // unsharded: the tree's last block draws z (MERKLE_TAIL_DRAW_Z)
     draw.op = MERKLE_TAIL_DRAW_Z;
     draw.coin_seed = dt_seed;
@@ -1355,7 +1382,7 @@ void ProofRun::constraint_stage() {
     draw.out = dt_zz;
     draw.pw = dt_pw;
     z_drawn = commit_rows(ctx, cm, 0, clde, n, C, logB, logn, R > 1, "ctree", ctree, T.constraint_root,
-                          /*fetch_root=*/false, &draw);
+                          /*fetch_root=*/false, &draw, derive ? &lc : nullptr);
   }
   croot_d = R > 1 ? ctree.top_d + 8 : ctree.nodes + 8;
   if (!z_drawn) launch_dt_draw_z(pf, st, dt_seed, croot_d, wn_root, logn, dt_zz, dt_pw);

@@ -86,8 +86,21 @@ struct MerkleTail {
   felt* out;
   felt* pw;
 };
+// The last composition column derived in the leaf pass instead of extended by an
+// NTT. On an LDE coset j that is also a CE coset (ce == B), x^n = kappa_j is
+// constant and H(x) = sum_c kappa_j^c H_c(x) (CompositionPoly splits H into C
+// columns of n coefficients), so H_{C-1}(x) = (H(x) - sum_{c<C-1} kappa_j^c H_c(x))
+// * kappa_j^-(C-1): C-1 products per row instead of one coset NTT per coset.
+// H = the constraint evaluations (H[jl*n + t], coset jl of the source), kap[2*jl]
+// = kappa, kap[2*jl+1] = kappa^-(C-1); the derived value is written to out[jl*n + t]
+// (the source's column C-1) and hashed with the row.
+struct LastCol {
+  const felt* H;
+  const felt* kap;
+  felt* out;
+};
 bool launch_merkle_lde(Prof& prof, hipStream_t s, const felt* lde, uint32_t cols, uint32_t logB, uint64_t n,
-                       uint32_t* nodes, uint64_t L, const MerkleTail* tail = nullptr);
+                       uint32_t* nodes, uint64_t L, const MerkleTail* tail = nullptr, const LastCol* lc = nullptr);
 // FRI layer tree over coset-major evaluations (B cosets of 16*m16): leaf r = j + B*t'
 bool launch_merkle_fri(Prof& prof, hipStream_t s, const felt* E, uint64_t m16, uint32_t logB, uint32_t F,
                        uint32_t* nodes, const MerkleTail* tail = nullptr);
@@ -99,7 +112,7 @@ bool merkle_upper(Prof& prof, hipStream_t s, uint32_t* nodes, uint64_t L, const 
 // all-to-all in 2^logK chunks along the destination rows: launch_leaf_hash_shard hashes chunk k
 void launch_leaf_hash_shard(Prof& prof, hipStream_t s, int mode, const felt* src, uint64_t n, uint32_t cols,
                             uint32_t logBl, uint32_t logrows, uint32_t logrr, uint32_t logK, uint32_t k,
-                            uint32_t* send);
+                            uint32_t* send, const LastCol* lc = nullptr);
 // sharded tree tops (R <= 64 subtree roots, all-gathered) -> top[1..2R) on the device,
 // then the tail's coin step on the root (tail nullable / MERKLE_TAIL_NONE: none)
 void launch_shard_top(Prof& prof, hipStream_t s, const uint32_t* roots, uint32_t R, uint32_t* top,
