@@ -102,6 +102,38 @@ def test_global_update_proof_bit_exact(ctx, ndev, n):
     assert verify_status(AIR_GLOBAL_UPDATE, gpu, felts_of(pub), opts) == 0  # product verifier
 
 
+@pytest.mark.parametrize("edit", ["row0", "transition", "last_row"])
+@pytest.mark.parametrize("device", [False, True])
+def test_global_update_pairing_edge_traces(ctx, edit, device):
+    """GlobalUpdate column pairing (columns 60+i derived from column i):
+    - row0: row 0 of column 60+i is unconstrained — still paired (c_i absorbs it);
+    - transition / last_row: a transition constraint fails on row 5 / row n-1, so the
+      prover must fall back to the unpaired proof.
+    Either way the GPU bytes equal the oracle's bytes for the same trace (the oracle
+    proves whatever trace it is given), from the host and the device-resident entry."""
+    opts = ProofOptions(40, 16, 8)
+    n = 256
+    p = gu_prover(30, n, opts, seed=7)
+    trace = p.build_trace()
+    pub_el = p.get_pub_inputs(trace).to_elements()
+    data = np.array(trace.data, copy=True)
+    row = {"row0": 0, "transition": 5, "last_row": n - 1}[edit]
+    data[61, row, 0] ^= np.uint64(0x5A5A)  # stays < p (low word only)
+    if device:
+        d = ctx.alloc(data.nbytes)
+        try:
+            ctx.to_device(d, data)
+            gpu, _ = ctx.prove_device(AIR_GLOBAL_UPDATE, d, 120, n, pub_el, opts)
+        finally:
+            ctx.free(d)
+    else:
+        gpu, _ = ctx.prove(AIR_GLOBAL_UPDATE, data, pub_el, opts)
+    ref, _ = O.prove(AIR_GLOBAL_UPDATE, data.tobytes(), 120, n, to_bytes(pub_el), opts)
+    assert gpu == ref
+    ok = O.verify(AIR_GLOBAL_UPDATE, gpu, to_bytes(pub_el), opts) == 0
+    assert ok == (edit == "row0")
+
+
 # ---------------------------------------------------------------- full-size configs
 @pytest.mark.slow
 def test_mimc_c2_full_size_bit_exact(ctx):

@@ -843,6 +843,72 @@ __global__ __launch_bounds__(TPB) void k_gu_tile_write(const felt* __restrict__ 
   }
 }
 
+// ---- GlobalUpdate column pairing. The transition constraints
+// k*next[i] - k*cur[i] - next[i+d] = 0 (src/aggregation/air.rs:118-125) fix
+// column d+i on rows 1..n-1 from column i, so as polynomials of degree < n
+//   T_{d+i}(X) = k*(T_i(X) - T_i(w_n^-1 X)) + c_i * L_0(X),
+//   c_i = T_{d+i}[0] - k*(T_i[0] - T_i[n-1]),  L_0(X) = (X^n - 1) / (n (X - 1)).
+// A trace that satisfies them (checked here, every row) gets the columns d..2d-1
+// of its coefficients and LDE from columns 0..d-1 at a few products per value
+// instead of an interpolation and B coset NTTs per column; the values are the
+// same field elements, so the proof bytes are too.
+
+// check rows 1..n-1 of the column pairs (c0+ci, d+c0+ci), ci < cw, of the natural
+// trace T (column-major); set *bad on any mismatch; c_i from row 0
+__global__ __launch_bounds__(TPB) void k_gu_check(const felt* __restrict__ T, uint32_t d, uint32_t logn, felt k,
+                                                  uint32_t c0, uint32_t cw, felt* __restrict__ cval,
+                                                  uint32_t* __restrict__ bad) {
+  const uint64_t n = 1ull << logn, q = blockIdx.x * (uint64_t)TPB + threadIdx.x;
+  if (q >= (uint64_t)cw << logn) return;
+  const uint32_t i = c0 + (uint32_t)(q >> logn);
+  const uint64_t t = q & (n - 1);
+  const felt* a = T + (uint64_t)i * n;
+  const felt* b = T + (uint64_t)(d + i) * n;
+  const felt prev = a[t == 0 ? n - 1 : t - 1];
+  const felt kd = mul(k, sub(a[t], prev));
+  if (t == 0) {
+    cval[i] = sub(b[0], kd);
+  } else if (!eq(b[t], kd)) {
+    *bad = 1u;
+  }
+}
+
+// coefficient columns (bit-reversed, scaled by n): coef_{d+i}[p] = k*(1 - w_n^-rev(p))*coef_i[p] + c_i
+__global__ __launch_bounds__(TPB) void k_gu_coef(felt* __restrict__ coef, uint32_t d, uint32_t logn, felt k,
+                                                 const felt* __restrict__ itwn, uint32_t c0, uint32_t cw,
+                                                 const felt* __restrict__ cval) {
+  const uint64_t n = 1ull << logn, p = blockIdx.x * (uint64_t)TPB + threadIdx.x;
+  if (p >= n) return;
+  const felt kw = mul(k, sub(one(), tw_full(itwn, rev_bits((uint32_t)p, logn), logn)));
+  for (uint32_t i = c0; i < c0 + cw; i++)
+    coef[(uint64_t)(d + i) * n + p] = add(mul(kw, coef[(uint64_t)i * n + p]), cval[i]);
+}
+
+// LDE columns over the cosets [0, Bl) (coset-major: column c at c*Bl*n, coset jl, row t):
+// lde_{d+i}(x) = k*(lde_i(x) - lde_i(w_n^-1 x)) + c_i*L_0(x), w_n^-1 x = the previous row of the coset
+__global__ __launch_bounds__(TPB) void k_gu_lde(felt* __restrict__ lde, uint32_t d, uint32_t logn, uint32_t logBl,
+                                                felt k, uint32_t c0, uint32_t cw, const felt* __restrict__ cval,
+                                                const felt* __restrict__ l0) {
+  const uint64_t n = 1ull << logn, q = blockIdx.x * (uint64_t)TPB + threadIdx.x;
+  if (q >= (n << logBl)) return;
+  const uint64_t t = q & (n - 1), qp = t == 0 ? q + n - 1 : q - 1;
+  const uint64_t cs = n << logBl;
+  const felt l = l0[q];
+  for (uint32_t i = c0; i < c0 + cw; i++) {
+    const felt* src = lde + (uint64_t)i * cs;
+    lde[(uint64_t)(d + i) * cs + q] = add(mul(k, sub(src[q], src[qp])), mul(cval[i], l));
+  }
+}
+
+// L_0(x) = (x^n - 1) / (n (x - 1)) over the points of a coset-major shard (domain-only table)
+__global__ __launch_bounds__(TPB) void k_l0_table(PointMap pm, uint64_t count, felt ninv, felt* __restrict__ out) {
+  const uint64_t q = blockIdx.x * (uint64_t)TPB + threadIdx.x;
+  if (q >= count) return;
+  const felt x = point_x(pm, q);
+  const felt xn = pow_u64(pm.cx[q >> pm.logn], 1ull << pm.logn);  // (c w_n^t)^n = c^n
+  out[q] = mul(mul(sub(xn, one()), ninv), inv(sub(x, one())));
+}
+
 }  // namespace
 
 // ======================================================================= host
@@ -1096,4 +1162,31 @@ void launch_dt_eval_consts(Prof& prof, hipStream_t s, int air, const felt* cc, f
                            const felt* zinv, uint32_t ce, uint32_t w, uint32_t num_t, felt* out) {
   LAUNCH(prof, "coin", s, 0.0,
          hipLaunchKernelGGL(k_dt_eval_consts, dim3(1), dim3(TPB), 0, s, air, cc, k, aval, zinv, ce, w, num_t, out));
+}
+
+void launch_gu_check(Prof& prof, hipStream_t s, const felt* T, uint32_t d, uint32_t logn, felt k, uint32_t c0,
+                     uint32_t cw, felt* cval, uint32_t* bad) {
+  const uint64_t cnt = (uint64_t)cw << logn;
+  LAUNCH(prof, "gu_pair", s, (double)cnt * 32.0,
+         hipLaunchKernelGGL(k_gu_check, dim3(blocks_for(cnt)), dim3(TPB), 0, s, T, d, logn, k, c0, cw, cval, bad));
+}
+
+void launch_gu_coef(Prof& prof, hipStream_t s, felt* coef, uint32_t d, uint32_t logn, felt k, const felt* itwn,
+                    uint32_t c0, uint32_t cw, const felt* cval) {
+  const uint64_t n = 1ull << logn;
+  LAUNCH(prof, "gu_pair", s, (double)n * cw * 32.0,
+         hipLaunchKernelGGL(k_gu_coef, dim3(blocks_for(n)), dim3(TPB), 0, s, coef, d, logn, k, itwn, c0, cw, cval));
+}
+
+void launch_gu_lde(Prof& prof, hipStream_t s, felt* lde, uint32_t d, uint32_t logn, uint32_t logBl, felt k,
+                   uint32_t c0, uint32_t cw, const felt* cval, const felt* l0) {
+  const uint64_t cnt = 1ull << (logn + logBl);
+  LAUNCH(prof, "gu_pair", s, (double)cnt * (cw * 32.0 + 16.0),
+         hipLaunchKernelGGL(k_gu_lde, dim3(blocks_for(cnt)), dim3(TPB), 0, s, lde, d, logn, logBl, k, c0, cw, cval,
+                            l0));
+}
+
+void launch_l0_table(Prof& prof, hipStream_t s, const PointMap& pm, uint64_t count, felt ninv, felt* out) {
+  LAUNCH(prof, "tables", s, (double)count * 16.0,
+         hipLaunchKernelGGL(k_l0_table, dim3(blocks_for(count)), dim3(TPB), 0, s, pm, count, ninv, out));
 }

@@ -1066,6 +1066,12 @@ struct ProofRun {
   unsigned long long dnonce = ~0ull;
   static constexpr uint64_t grind_chunk = 1ull << 22;
   uint64_t nonce = 0;
+  // GlobalUpdate column pairing (trace_stage): world 1 only
+  bool allow_pair = true, paired = false;
+  felt* gu_cval = nullptr;
+  uint32_t* gu_bad = nullptr;
+  const felt* l0_table();
+  bool pair_failed();
 
   ProofRun(zkp_ctx* c, zkp_comm* m, const zkp_proof_options* opts)
       : ctx(c), cm(m), o(opts), st(c->stream), pf(c->prof) {
@@ -1125,6 +1131,8 @@ int ProofRun::init(int air_id, const felt* d_trace_in, uint32_t width, uint64_t 
   while (u0 + cel < ce && ce_owner(u0 + cel) == rank) cel++;
   celmax = ce >= R ? ce / R : 1;
   g = felt_u64(3);
+  static const bool no_pair = getenv("ZKP_NO_GU_PAIR") != nullptr;  // A/B switch
+  paired = allow_pair && !no_pair && air.id == ZKP_AIR_GLOBAL_UPDATE && R == 1 && w == 2 * GU_D;
   ood_trace.assign(2 * (size_t)w, felt{});
   ood_comp.assign(C, felt{});
   return 0;
@@ -1242,19 +1250,43 @@ void ProofRun::trace_stage(const zkp_felt* h_trace) {
     // the groups grow geometrically (x1.5 from ~w/40 columns: C3 3, 4, 6, ..., 38),
     // so only the small first group's upload is exposed and every later one hides
     // behind the previous group's LDE (a column's upload takes ~0.55x its LDE at C3)
-    std::vector<std::pair<uint32_t, uint32_t>> grp;  // (first column, columns)
+    // GlobalUpdate column pairing (k_gu_check): only columns [0, d)
+    // are interpolated and extended; column d+i is checked against its transition
+    // constraint and derived from column i in the same group (its upload rides
+    // with column i's). A trace that fails the check is proven again unpaired
+    // (prove_impl), so the result never depends on the shortcut.
+    const uint32_t d = paired ? w / 2 : w;
+    if (paired) {
+      gu_cval = ctx->buf<felt>("gu_cval", d);
+      gu_bad = ctx->buf<uint32_t>("gu_bad", 1);
+      HIP_CHECK(hipMemsetAsync(gu_bad, 0, 4, st));
+    }
+    // groups (first column, columns): one for device-resident traces. Host traces
+    // upload group g+1 on the copy stream while the main stream works on group g.
+    // Columns [0, d): interpolation + coset LDE, the groups growing geometrically
+    // (x1.5 from ~w/40 columns: C3 unpaired 3, 4, 6, ..., 38), so only the small
+    // first group's upload is exposed and every later one hides behind the previous
+    // group's LDE (a column uploads in ~0.55x its LDE at C3). Paired columns
+    // [d, w) follow in equal groups of ~d/10: their derivation is ~5x cheaper than
+    // an LDE, so the upload is the critical path there and a small last group
+    // leaves little after it.
+    std::vector<std::pair<uint32_t, uint32_t>> grp;
     static const uint32_t growth =  // percent (A/B switch ZKP_UPLOAD_GROWTH)
         getenv("ZKP_UPLOAD_GROWTH") ? std::max(110, atoi(getenv("ZKP_UPLOAD_GROWTH"))) : 150u;
-    if (h_trace && w >= 4) {
+    if (h_trace && d >= 4) {
       uint32_t cw = std::max(1u, w / 40);
-      for (uint32_t c = 0; c < w;) {
-        cw = std::min(cw, w - c);
+      for (uint32_t c = 0; c < d;) {
+        cw = std::min(cw, d - c);
         grp.push_back({c, cw});
         c += cw;
         cw = std::max(cw + 1, cw * growth / 100);
       }
     } else {
-      grp.push_back({0u, w});
+      grp.push_back({0u, d});
+    }
+    if (paired) {
+      const uint32_t pw = h_trace ? std::max(1u, d / 10) : d;
+      for (uint32_t c = d; c < w; c += pw) grp.push_back({c, std::min(pw, w - c)});
     }
     const bool piped = h_trace && grp.size() > 1;
     if (piped) {  // the copy stream starts after everything already queued
@@ -1270,8 +1302,15 @@ void ProofRun::trace_stage(const zkp_felt* h_trace) {
                                  ctx->side));
         HIP_CHECK(hipEventRecord(ctx->up_ev[g], ctx->side));
         HIP_CHECK(hipStreamWaitEvent(st, ctx->up_ev[g], 0));
-      } else if (h_trace) {
+      } else if (h_trace && g == 0) {
         ctx->upload(dcol, h_trace, (size_t)w * n * 16);
+      }
+      if (c0 >= d) {  // paired columns d+i, i in [c0 - d, c0 - d + cw): check, then derive
+        const uint32_t i0 = c0 - d;
+        launch_gu_check(pf, st, d_trace, d, logn, air.k, i0, cw, gu_cval, gu_bad);
+        launch_gu_coef(pf, st, coef, d, logn, air.k, ctx->itws(logN) + ((n >> 1) - 1), i0, cw, gu_cval);
+        launch_gu_lde(pf, st, tlde, d, logn, logBl, air.k, i0, cw, gu_cval, l0_table());
+        continue;
       }
       NttBatch ib{dcol, coef + (size_t)c0 * n, nullptr, n, n, 1, 1, cw};
       launch_ntt(pf, st, ib, logn, false, ctx->itws(logN), logN);
@@ -1770,23 +1809,49 @@ int ProofRun::finish(uint8_t** proof, uint64_t* proof_len, zkp_transcript* tr_ou
   return 0;
 }
 
+// L_0 over this rank's LDE cosets (domain-only: cached per (n, B, j0, Bl))
+const felt* ProofRun::l0_table() {
+  const std::string key = "l0_" + std::to_string(logn) + "_" + std::to_string(logB) + "_" + std::to_string(j0) + "_" +
+                          std::to_string(Bl);
+  felt* t = ctx->buf<felt>(key, (size_t)Bl * n);
+  if (!ctx->have_cached(key)) launch_l0_table(pf, st, PointMap{cx + j0, twn, logn}, (uint64_t)Bl * n, inv(felt_u64(n)), t);
+  return t;
+}
+
+// a paired trace whose transitions did not hold (one 4-byte read after the proof's last kernels)
+bool ProofRun::pair_failed() {
+  if (!paired) return false;
+  uint32_t bad = 0;
+  ctx->download(&bad, gu_bad, 4);
+  return bad != 0;
+}
+
 // h_trace (nullable): the trace is still in host memory and d_trace is its
 // device buffer; the upload is pipelined with the trace interpolation and LDE
 // by column groups (wide traces), so PCIe overlaps the first stage's kernels.
 int prove_impl(zkp_ctx* ctx, zkp_comm* cm, int air_id, const felt* d_trace, uint32_t w, uint64_t n,
                const zkp_felt* pub_elems, uint64_t n_pub, const zkp_proof_options* o, uint8_t** proof,
                uint64_t* proof_len, zkp_transcript* tr_out, const zkp_felt* h_trace = nullptr) {
-  ProofRun run(ctx, cm, o);
-  int rc = run.init(air_id, d_trace, w, n, pub_elems, n_pub, proof, proof_len);
-  if (rc) return rc;
-  run.setup();
-  run.trace_stage(h_trace);
-  run.constraint_stage();
-  run.ood_stage();
-  run.deep_stage();
-  run.fri_stage();
-  run.grind_stage();
-  return run.finish(proof, proof_len, tr_out);
+  for (int attempt = 0;; attempt++) {
+    ProofRun run(ctx, cm, o);
+    run.allow_pair = attempt == 0;
+    int rc = run.init(air_id, d_trace, w, n, pub_elems, n_pub, proof, proof_len);
+    if (rc) return rc;
+    run.setup();
+    run.trace_stage(h_trace);
+    run.constraint_stage();
+    run.ood_stage();
+    run.deep_stage();
+    run.fri_stage();
+    run.grind_stage();
+    // the paired columns rest on the trace's transitions: if they do not hold, prove
+    // the (now device-resident) trace again without the pairing
+    if (run.pair_failed()) {
+      h_trace = nullptr;
+      continue;
+    }
+    return run.finish(proof, proof_len, tr_out);
+  }
 }
 
 template <typename F>

@@ -246,6 +246,19 @@ void launch_lin_lincomb(Prof& prof, hipStream_t s, bool trans, bool two, const f
 void launch_eval_linear_pts(Prof& prof, hipStream_t s, const EvalCommon& c, const LinearEvalArgs& a, const felt* ev,
                             felt* comp);
 
+// GlobalUpdate column pairing (kernels.hip): columns d+i from columns i < d for a
+// trace whose transitions hold. check: rows 1..n-1 of pairs c0..c0+cw of the natural
+// trace (*bad = 1 on a mismatch) and c_i from row 0; coef: the derived coefficient
+// columns (itwn = the inverse w_n table level); lde: the derived LDE columns over Bl
+// cosets (l0 = L_0 over those cosets, launch_l0_table)
+void launch_gu_check(Prof& prof, hipStream_t s, const felt* T, uint32_t d, uint32_t logn, felt k, uint32_t c0,
+                     uint32_t cw, felt* cval, uint32_t* bad);
+void launch_gu_coef(Prof& prof, hipStream_t s, felt* coef, uint32_t d, uint32_t logn, felt k, const felt* itwn,
+                    uint32_t c0, uint32_t cw, const felt* cval);
+void launch_gu_lde(Prof& prof, hipStream_t s, felt* lde, uint32_t d, uint32_t logn, uint32_t logBl, felt k,
+                   uint32_t c0, uint32_t cw, const felt* cval, const felt* l0);
+void launch_l0_table(Prof& prof, hipStream_t s, const PointMap& pm, uint64_t count, felt ninv, felt* out);
+
 // composition polynomial from CE-coset interpolations (see kernels.hip): for the
 // bit-reversed positions [p0, p0 + nR), n * c_m = (sum_u Si_u * W_u * w_ce^-um) * g^-mn / ce;
 // consts = [g^-mn / ce for m < C | w_ce^-k for k < ce/2] (ce in {2, 4, 8, 16})
