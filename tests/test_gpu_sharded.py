@@ -53,6 +53,30 @@ def test_mimc_sharded_matches_oracle(rank_ctxs):
 
 
 @pytest.mark.parametrize("world", [2, 4, 8])
+@pytest.mark.parametrize("n,edit", [(1 << 11, None), (1 << 13, None), (1 << 13, "transition"), (1 << 11, "row0")])
+def test_global_update_sharded_device_paired(ctx, rank_ctxs, world, n, edit):
+    """Sharded device-resident GlobalUpdate traces take the column pairing (each rank
+    checks 1/R of the rows, flags all-gathered; derived coefficients over the rank's
+    position slice when the OOD is split — n = 2^13 at world 2/4 — else all). A failed
+    transition falls back to the unpaired proof on every rank. Bytes = single GPU."""
+    opts = ProofOptions.reference()
+    p = gu_prover(16, n, opts, seed=world + n)
+    trace = p.build_trace()
+    pub = p.get_pub_inputs(trace).to_elements()
+    data = np.array(trace.data, copy=True)
+    if edit:
+        data[75, 0 if edit == "row0" else n // 2 + 3, 0] ^= np.uint64(0x1234)
+    ref, _ = ctx.prove(AIR_GLOBAL_UPDATE, data, pub, opts)
+    d = ctx.alloc(data.nbytes)
+    try:
+        ctx.to_device(d, data)
+        res = prove_local_group(world, AIR_GLOBAL_UPDATE, d, pub, opts, contexts=rank_ctxs[:world], shape=(120, n))
+    finally:
+        ctx.free(d)
+    check_all_equal(res, ref)
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_global_update_sharded_equals_single(ctx, rank_ctxs, world):
     # ce = 2 < world for 4 and 8: only two ranks hold constraint-evaluation cosets
     opts = ProofOptions.reference()

@@ -853,15 +853,16 @@ __global__ __launch_bounds__(TPB) void k_gu_tile_write(const felt* __restrict__ 
 // instead of an interpolation and B coset NTTs per column; the values are the
 // same field elements, so the proof bytes are too.
 
-// check rows 1..n-1 of the column pairs (c0+ci, d+c0+ci), ci < cw, of the natural
-// trace T (column-major); set *bad on any mismatch; c_i from row 0
+// check rows [t0, t0 + 2^logtn) (row 0 excepted) of the column pairs (c0+ci, d+c0+ci),
+// ci < cw, of the natural trace T (column-major); set *bad on any mismatch; c_i
+// when the rows include row 0
 __global__ __launch_bounds__(TPB) void k_gu_check(const felt* __restrict__ T, uint32_t d, uint32_t logn, felt k,
-                                                  uint32_t c0, uint32_t cw, felt* __restrict__ cval,
-                                                  uint32_t* __restrict__ bad) {
+                                                  uint32_t c0, uint32_t cw, uint64_t t0, uint32_t logtn,
+                                                  felt* __restrict__ cval, uint32_t* __restrict__ bad) {
   const uint64_t n = 1ull << logn, q = blockIdx.x * (uint64_t)TPB + threadIdx.x;
-  if (q >= (uint64_t)cw << logn) return;
-  const uint32_t i = c0 + (uint32_t)(q >> logn);
-  const uint64_t t = q & (n - 1);
+  if (q >= (uint64_t)cw << logtn) return;
+  const uint32_t i = c0 + (uint32_t)(q >> logtn);
+  const uint64_t t = t0 + (q & ((1ull << logtn) - 1));
   const felt* a = T + (uint64_t)i * n;
   const felt* b = T + (uint64_t)(d + i) * n;
   const felt prev = a[t == 0 ? n - 1 : t - 1];
@@ -873,12 +874,13 @@ __global__ __launch_bounds__(TPB) void k_gu_check(const felt* __restrict__ T, ui
   }
 }
 
-// coefficient columns (bit-reversed, scaled by n): coef_{d+i}[p] = k*(1 - w_n^-rev(p))*coef_i[p] + c_i
+// coefficient columns (bit-reversed, scaled by n) at the positions [p0, p0 + np):
+// coef_{d+i}[p] = k*(1 - w_n^-rev(p))*coef_i[p] + c_i
 __global__ __launch_bounds__(TPB) void k_gu_coef(felt* __restrict__ coef, uint32_t d, uint32_t logn, felt k,
                                                  const felt* __restrict__ itwn, uint32_t c0, uint32_t cw,
-                                                 const felt* __restrict__ cval) {
-  const uint64_t n = 1ull << logn, p = blockIdx.x * (uint64_t)TPB + threadIdx.x;
-  if (p >= n) return;
+                                                 uint64_t p0, uint64_t np, const felt* __restrict__ cval) {
+  const uint64_t n = 1ull << logn, p = p0 + blockIdx.x * (uint64_t)TPB + threadIdx.x;
+  if (p >= p0 + np) return;
   const felt kw = mul(k, sub(one(), tw_full(itwn, rev_bits((uint32_t)p, logn), logn)));
   for (uint32_t i = c0; i < c0 + cw; i++)
     coef[(uint64_t)(d + i) * n + p] = add(mul(kw, coef[(uint64_t)i * n + p]), cval[i]);
@@ -1165,17 +1167,18 @@ void launch_dt_eval_consts(Prof& prof, hipStream_t s, int air, const felt* cc, f
 }
 
 void launch_gu_check(Prof& prof, hipStream_t s, const felt* T, uint32_t d, uint32_t logn, felt k, uint32_t c0,
-                     uint32_t cw, felt* cval, uint32_t* bad) {
-  const uint64_t cnt = (uint64_t)cw << logn;
+                     uint32_t cw, uint64_t t0, uint32_t logtn, felt* cval, uint32_t* bad) {
+  const uint64_t cnt = (uint64_t)cw << logtn;
   LAUNCH(prof, "gu_pair", s, (double)cnt * 32.0,
-         hipLaunchKernelGGL(k_gu_check, dim3(blocks_for(cnt)), dim3(TPB), 0, s, T, d, logn, k, c0, cw, cval, bad));
+         hipLaunchKernelGGL(k_gu_check, dim3(blocks_for(cnt)), dim3(TPB), 0, s, T, d, logn, k, c0, cw, t0, logtn,
+                            cval, bad));
 }
 
 void launch_gu_coef(Prof& prof, hipStream_t s, felt* coef, uint32_t d, uint32_t logn, felt k, const felt* itwn,
-                    uint32_t c0, uint32_t cw, const felt* cval) {
-  const uint64_t n = 1ull << logn;
-  LAUNCH(prof, "gu_pair", s, (double)n * cw * 32.0,
-         hipLaunchKernelGGL(k_gu_coef, dim3(blocks_for(n)), dim3(TPB), 0, s, coef, d, logn, k, itwn, c0, cw, cval));
+                    uint32_t c0, uint32_t cw, uint64_t p0, uint64_t np, const felt* cval) {
+  LAUNCH(prof, "gu_pair", s, (double)np * cw * 32.0,
+         hipLaunchKernelGGL(k_gu_coef, dim3(blocks_for(np)), dim3(TPB), 0, s, coef, d, logn, k, itwn, c0, cw, p0, np,
+                            cval));
 }
 
 void launch_gu_lde(Prof& prof, hipStream_t s, felt* lde, uint32_t d, uint32_t logn, uint32_t logBl, felt k,

@@ -1069,7 +1069,8 @@ struct ProofRun {
   // GlobalUpdate column pairing (trace_stage): world 1 only
   bool allow_pair = true, paired = false;
   felt* gu_cval = nullptr;
-  uint32_t* gu_bad = nullptr;
+  uint32_t* gu_bad = nullptr;    // this rank's check flag (4 words)
+  uint32_t* gu_flags = nullptr;  // column-sharded: every rank's flags (all-gathered)
   const felt* l0_table();
   bool pair_failed();
 
@@ -1131,8 +1132,6 @@ int ProofRun::init(int air_id, const felt* d_trace_in, uint32_t width, uint64_t 
   while (u0 + cel < ce && ce_owner(u0 + cel) == rank) cel++;
   celmax = ce >= R ? ce / R : 1;
   g = felt_u64(3);
-  static const bool no_pair = getenv("ZKP_NO_GU_PAIR") != nullptr;  // A/B switch
-  paired = allow_pair && !no_pair && air.id == ZKP_AIR_GLOBAL_UPDATE && R == 1 && w == 2 * GU_D;
   ood_trace.assign(2 * (size_t)w, felt{});
   ood_comp.assign(C, felt{});
   return 0;
@@ -1183,9 +1182,25 @@ void ProofRun::trace_stage(const zkp_felt* h_trace) {
   coef = ctx->buf<felt>("coef", (size_t)(w + C) * n);
   tlde = ctx->buf<felt>("tlde", (size_t)w * Bl * n);
   bool coeffs_drawn = false;
+  // GlobalUpdate column pairing (k_gu_check): only columns [0, wi)
+  // are interpolated and extended; column d+i >= wi is checked against its
+  // transition constraint and derived from column i. A trace that fails the check
+  // is proven again unpaired (prove_impl), so the result never depends on the
+  // shortcut. Sharded proofs pair device-resident traces (every rank holds the
+  // whole trace; a host trace uploads only the rank's share).
+  static const bool no_pair = getenv("ZKP_NO_GU_PAIR") != nullptr;  // A/B switch
+  paired = allow_pair && !no_pair && air.id == ZKP_AIR_GLOBAL_UPDATE && w == 2 * GU_D && (R == 1 || !h_trace);
+  const uint32_t d = w / 2;
   // wide traces shard the interpolation by column (cpt columns per rank) when the
   // width divides over the ranks; narrow ones interpolate on every rank
-  const uint32_t cpt = (R > 1 && w % R == 0 && w >= 2 * R) ? w / R : 0;
+  uint32_t wi = paired && R > 1 ? (d + R - 1) / R * R : w;
+  uint32_t cpt = (R > 1 && wi % R == 0 && wi >= 2 * R && wi <= w) ? wi / R : 0;
+  if (R > 1 && !cpt) wi = w, cpt = (w % R == 0 && w >= 2 * R) ? w / R : 0;
+  if (paired) {
+    gu_cval = ctx->buf<felt>("gu_cval", d);
+    gu_bad = ctx->buf<uint32_t>("gu_bad", 4);
+    HIP_CHECK(hipMemsetAsync(gu_bad, 0, 16, st));
+  }
   if (cpt) {
     // column-sharded interpolation: in round k rank r interpolates
     // columns [k*R*cpr + r*cpr, +cpr) — uploading only those columns of a host
@@ -1224,6 +1239,25 @@ void ProofRun::trace_stage(const zkp_felt* h_trace) {
     // nothing on the copy stream may outlive the stage (the next proof reuses its buffers)
     HIP_CHECK(hipEventRecord(ctx->up_ev[2 * K], ctx->copy));
     HIP_CHECK(hipStreamWaitEvent(st, ctx->up_ev[2 * K], 0));
+    if (paired && wi < w) {
+      // derived columns [wi, w) from [i0, i0 + np): each rank checks its 1/R of the
+      // rows (the flags are all-gathered; every rank computes c_i from row 0), derives
+      // the coefficients its consumers read (the OOD blocks and the lincombs take
+      // the positions [rank*nR, +nR) when the OOD is split, else all) and the LDE
+      // of its cosets from its own extended columns
+      const uint32_t i0 = wi - d, np = w - wi;
+      const uint64_t nR = n >> logR;
+      launch_gu_check(pf, st, d_trace, d, logn, air.k, i0, np, (uint64_t)rank * nR, logn - logR, gu_cval, gu_bad);
+      if (rank) launch_gu_check(pf, st, d_trace, d, logn, air.k, i0, np, 0, 0, gu_cval, gu_bad);
+      gu_flags = ctx->buf<uint32_t>("gu_flags", 4 * (size_t)R);
+      cm->all_gather(st, gu_bad, gu_flags, 16);
+      const bool slice = (n >> std::min(logn, 11u)) >= R;  // ood_launch splits its blocks
+      launch_gu_coef(pf, st, coef, d, logn, air.k, ctx->itws(logN) + ((n >> 1) - 1), i0, np,
+                     slice ? (uint64_t)rank * nR : 0, slice ? nR : n, gu_cval);
+      launch_gu_lde(pf, st, tlde, d, logn, logBl, air.k, i0, np, gu_cval, l0_table());
+    } else {
+      paired = false;
+    }
   } else {
     if (h_trace && R > 1) {
       // sharded host trace: each rank uploads only its 1/R row
@@ -1255,12 +1289,7 @@ void ProofRun::trace_stage(const zkp_felt* h_trace) {
     // constraint and derived from column i in the same group (its upload rides
     // with column i's). A trace that fails the check is proven again unpaired
     // (prove_impl), so the result never depends on the shortcut.
-    const uint32_t d = paired ? w / 2 : w;
-    if (paired) {
-      gu_cval = ctx->buf<felt>("gu_cval", d);
-      gu_bad = ctx->buf<uint32_t>("gu_bad", 1);
-      HIP_CHECK(hipMemsetAsync(gu_bad, 0, 4, st));
-    }
+    const uint32_t wd = paired ? d : w;  // columns interpolated and extended here
     // groups (first column, columns): one for device-resident traces. Host traces
     // upload group g+1 on the copy stream while the main stream works on group g.
     // Columns [0, d): interpolation + coset LDE, the groups growing geometrically
@@ -1273,16 +1302,16 @@ void ProofRun::trace_stage(const zkp_felt* h_trace) {
     std::vector<std::pair<uint32_t, uint32_t>> grp;
     static const uint32_t growth =  // percent (A/B switch ZKP_UPLOAD_GROWTH)
         getenv("ZKP_UPLOAD_GROWTH") ? std::max(110, atoi(getenv("ZKP_UPLOAD_GROWTH"))) : 150u;
-    if (h_trace && d >= 4) {
+    if (h_trace && wd >= 4) {
       uint32_t cw = std::max(1u, w / 40);
-      for (uint32_t c = 0; c < d;) {
-        cw = std::min(cw, d - c);
+      for (uint32_t c = 0; c < wd;) {
+        cw = std::min(cw, wd - c);
         grp.push_back({c, cw});
         c += cw;
         cw = std::max(cw + 1, cw * growth / 100);
       }
     } else {
-      grp.push_back({0u, d});
+      grp.push_back({0u, wd});
     }
     if (paired) {
       const uint32_t pw = h_trace ? std::max(1u, d / 10) : d;
@@ -1305,10 +1334,10 @@ void ProofRun::trace_stage(const zkp_felt* h_trace) {
       } else if (h_trace && g == 0) {
         ctx->upload(dcol, h_trace, (size_t)w * n * 16);
       }
-      if (c0 >= d) {  // paired columns d+i, i in [c0 - d, c0 - d + cw): check, then derive
+      if (c0 >= wd) {  // paired columns d+i, i in [c0 - d, c0 - d + cw): check, then derive
         const uint32_t i0 = c0 - d;
-        launch_gu_check(pf, st, d_trace, d, logn, air.k, i0, cw, gu_cval, gu_bad);
-        launch_gu_coef(pf, st, coef, d, logn, air.k, ctx->itws(logN) + ((n >> 1) - 1), i0, cw, gu_cval);
+        launch_gu_check(pf, st, d_trace, d, logn, air.k, i0, cw, 0, logn, gu_cval, gu_bad);
+        launch_gu_coef(pf, st, coef, d, logn, air.k, ctx->itws(logN) + ((n >> 1) - 1), i0, cw, 0, n, gu_cval);
         launch_gu_lde(pf, st, tlde, d, logn, logBl, air.k, i0, cw, gu_cval, l0_table());
         continue;
       }
@@ -1821,9 +1850,11 @@ const felt* ProofRun::l0_table() {
 // a paired trace whose transitions did not hold (one 4-byte read after the proof's last kernels)
 bool ProofRun::pair_failed() {
   if (!paired) return false;
-  uint32_t bad = 0;
-  ctx->download(&bad, gu_bad, 4);
-  return bad != 0;
+  std::vector<uint32_t> f(gu_flags ? 4 * (size_t)R : 4);
+  ctx->download(f.data(), gu_flags ? gu_flags : gu_bad, f.size() * 4);
+  for (uint32_t v : f)
+    if (v) return true;
+  return false;
 }
 
 // h_trace (nullable): the trace is still in host memory and d_trace is its

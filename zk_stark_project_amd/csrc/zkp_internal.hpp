@@ -247,14 +247,15 @@ void launch_eval_linear_pts(Prof& prof, hipStream_t s, const EvalCommon& c, cons
                             felt* comp);
 
 // GlobalUpdate column pairing (kernels.hip): columns d+i from columns i < d for a
-// trace whose transitions hold. check: rows 1..n-1 of pairs c0..c0+cw of the natural
-// trace (*bad = 1 on a mismatch) and c_i from row 0; coef: the derived coefficient
-// columns (itwn = the inverse w_n table level); lde: the derived LDE columns over Bl
-// cosets (l0 = L_0 over those cosets, launch_l0_table)
+// trace whose transitions hold. check: rows [t0, t0 + 2^logtn) of pairs c0..c0+cw of
+// the natural trace (*bad = 1 on a mismatch; row 0 gives c_i); coef: the derived
+// coefficient columns at positions [p0, p0 + np) (itwn = the inverse w_n table
+// level); lde: the derived LDE columns over Bl cosets (l0 = L_0 over those cosets,
+// launch_l0_table)
 void launch_gu_check(Prof& prof, hipStream_t s, const felt* T, uint32_t d, uint32_t logn, felt k, uint32_t c0,
-                     uint32_t cw, felt* cval, uint32_t* bad);
+                     uint32_t cw, uint64_t t0, uint32_t logtn, felt* cval, uint32_t* bad);
 void launch_gu_coef(Prof& prof, hipStream_t s, felt* coef, uint32_t d, uint32_t logn, felt k, const felt* itwn,
-                    uint32_t c0, uint32_t cw, const felt* cval);
+                    uint32_t c0, uint32_t cw, uint64_t p0, uint64_t np, const felt* cval);
 void launch_gu_lde(Prof& prof, hipStream_t s, felt* lde, uint32_t d, uint32_t logn, uint32_t logBl, felt k,
                    uint32_t c0, uint32_t cw, const felt* cval, const felt* l0);
 void launch_l0_table(Prof& prof, hipStream_t s, const PointMap& pm, uint64_t count, felt ninv, felt* out);
