@@ -75,15 +75,32 @@ def test_mimc_proof_bit_exact(ctx, n, blowup, q, grind):
     assert verify_status(AIR_MIMC, gpu, felts_of(pub), opts) == 0  # product verifier
 
 
-def gu_prover(ndev, n, opts, seed):
+def gu_prover(ndev, n, opts, seed, k=None):
     rnd = random.Random(seed)
     r = lambda: rnd.randrange(2**64)
     gw = [[r() for _ in range(9)] for _ in range(6)]
     gb = [r() for _ in range(6)]
     lw = [[[r() for _ in range(9)] for _ in range(6)] for _ in range(ndev)]
     lb = [[r() for _ in range(6)] for _ in range(ndev)]
-    return GlobalUpdateProver(opts, gw, gb, lw, lb, f64_to_felt(ndev), trace_length=n,
+    return GlobalUpdateProver(opts, gw, gb, lw, lb, f64_to_felt(ndev) if k is None else k, trace_length=n,
                               blinding=[r() for _ in range(60)])
+
+
+@pytest.mark.parametrize("k", [0, 1, (1 << 32) - 1, 1 << 32, P - 1, (1 << 100) + 12345])
+def test_global_update_k_values(ctx, k):
+    """The paired columns multiply by the AIR's k: a 32-bit k takes the short product
+    (fpd::mul_u32), any other the full one; k = 0 makes the paired columns constant
+    after row 0. GPU bytes == oracle bytes for each."""
+    opts = ProofOptions(40, 16, 8)
+    n = 256
+    p = gu_prover(20, n, opts, seed=11, k=k)
+    trace = p.build_trace()
+    pub_el = p.get_pub_inputs(trace).to_elements()
+    gpu, _ = ctx.prove(AIR_GLOBAL_UPDATE, trace.data, pub_el, opts)
+    ref, _ = O.prove(AIR_GLOBAL_UPDATE, trace.to_bytes(), 120, n, to_bytes(pub_el), opts)
+    assert gpu == ref
+    if k:  # k = 0: the builder's k^-1 = 0 need not give a valid trace (then it is proven unpaired)
+        assert O.verify(AIR_GLOBAL_UPDATE, gpu, to_bytes(pub_el), opts) == 0
 
 
 @pytest.mark.parametrize("ndev,n", [(2, 8), (6, 64), (30, 256), (64, 1 << 12)])

@@ -185,6 +185,14 @@ ZKP_HD felt mul(felt a, felt b) {
   return mul_host(a, b);
 #endif
 }
+// a * k for a 32-bit k (fpd::mul_u32 on the device)
+ZKP_HD felt mul_u32(felt a, uint32_t k) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return fpd::mul_u32(a, k);
+#else
+  return mul_host(a, make(k, 0));
+#endif
+}
 ZKP_HD felt neg(felt a) { return sub(zero(), a); }
 ZKP_HD felt sqr(felt a) { return mul(a, a); }
 

@@ -844,7 +844,7 @@ __global__ __launch_bounds__(TPB) void k_gu_tile_write(const felt* __restrict__ 
 }
 
 // ---- GlobalUpdate column pairing. The transition constraints
-// k*next[i] - k*cur[i] - next[i+d] = 0 (src/aggregation/air.rs:118-125) fix
+// k*next[i] - k*cur[i] - next[i+d] = 0 (src/aggregation/air.rs:101-119) fix
 // column d+i on rows 1..n-1 from column i, so as polynomials of degree < n
 //   T_{d+i}(X) = k*(T_i(X) - T_i(w_n^-1 X)) + c_i * L_0(X),
 //   c_i = T_{d+i}[0] - k*(T_i[0] - T_i[n-1]),  L_0(X) = (X^n - 1) / (n (X - 1)).
@@ -888,6 +888,8 @@ __global__ __launch_bounds__(TPB) void k_gu_coef(felt* __restrict__ coef, uint32
 
 // LDE columns over the cosets [0, Bl) (coset-major: column c at c*Bl*n, coset jl, row t):
 // lde_{d+i}(x) = k*(lde_i(x) - lde_i(w_n^-1 x)) + c_i*L_0(x), w_n^-1 x = the previous row of the coset
+// SMALLK: k < 2^32 (the reference's k = devices * 10^6), multiplied with mul_u32
+template <bool SMALLK>
 __global__ __launch_bounds__(TPB) void k_gu_lde(felt* __restrict__ lde, uint32_t d, uint32_t logn, uint32_t logBl,
                                                 felt k, uint32_t c0, uint32_t cw, const felt* __restrict__ cval,
                                                 const felt* __restrict__ l0) {
@@ -898,8 +900,30 @@ __global__ __launch_bounds__(TPB) void k_gu_lde(felt* __restrict__ lde, uint32_t
   const felt l = l0[q];
   for (uint32_t i = c0; i < c0 + cw; i++) {
     const felt* src = lde + (uint64_t)i * cs;
-    lde[(uint64_t)(d + i) * cs + q] = add(mul(k, sub(src[q], src[qp])), mul(cval[i], l));
+    const felt df = sub(src[q], src[qp]);
+    const felt kd = SMALLK ? mul_u32(df, (uint32_t)k.lo) : mul(k, df);
+    lde[(uint64_t)(d + i) * cs + q] = add(kd, mul(cval[i], l));
   }
+}
+
+// the lazy paired columns [wi, w) of the queried rows held here (GuLazy): thread per
+// (position, column)
+__global__ __launch_bounds__(TPB) void k_gu_fill(felt* __restrict__ lde, uint32_t w, uint32_t logn, uint32_t logB,
+                                                 uint32_t j0, uint32_t logBl, const uint64_t* __restrict__ pos,
+                                                 uint32_t npos, GuLazy gl) {
+  const uint32_t nc = w - gl.wi;
+  const uint64_t q = blockIdx.x * (uint64_t)TPB + threadIdx.x;
+  if (q >= (uint64_t)npos * nc) return;
+  const uint64_t i = pos[q / nc];
+  const uint32_t c = gl.wi + (uint32_t)(q % nc);
+  const uint64_t n = 1ull << logn, j = i & ((1ull << logB) - 1), t = i >> logB;
+  if (j < j0 || j >= j0 + (1ull << logBl)) return;
+  const uint64_t jl = j - j0, cstride = n << logBl;
+  const felt* base = lde + jl * n + t;
+  const felt* prev = lde + jl * n + (t == 0 ? n - 1 : t - 1);
+  const uint32_t ic = c - gl.d;
+  const felt v = add(mul(gl.k, sub(base[ic * cstride], prev[ic * cstride])), mul(gl.cval[ic], gl.l0[jl * n + t]));
+  lde[c * cstride + jl * n + t] = v;
 }
 
 // L_0(x) = (x^n - 1) / (n (x - 1)) over the points of a coset-major shard (domain-only table)
@@ -1184,12 +1208,27 @@ void launch_gu_coef(Prof& prof, hipStream_t s, felt* coef, uint32_t d, uint32_t 
 void launch_gu_lde(Prof& prof, hipStream_t s, felt* lde, uint32_t d, uint32_t logn, uint32_t logBl, felt k,
                    uint32_t c0, uint32_t cw, const felt* cval, const felt* l0) {
   const uint64_t cnt = 1ull << (logn + logBl);
-  LAUNCH(prof, "gu_pair", s, (double)cnt * (cw * 32.0 + 16.0),
-         hipLaunchKernelGGL(k_gu_lde, dim3(blocks_for(cnt)), dim3(TPB), 0, s, lde, d, logn, logBl, k, c0, cw, cval,
-                            l0));
+  const bool smallk = k.hi == 0 && (k.lo >> 32) == 0;
+  if (smallk)
+    LAUNCH(prof, "gu_pair", s, (double)cnt * (cw * 32.0 + 16.0),
+           hipLaunchKernelGGL(k_gu_lde<true>, dim3(blocks_for(cnt)), dim3(TPB), 0, s, lde, d, logn, logBl, k, c0, cw,
+                              cval, l0));
+  else
+    LAUNCH(prof, "gu_pair", s, (double)cnt * (cw * 32.0 + 16.0),
+           hipLaunchKernelGGL(k_gu_lde<false>, dim3(blocks_for(cnt)), dim3(TPB), 0, s, lde, d, logn, logBl, k, c0, cw,
+                              cval, l0));
 }
 
 void launch_l0_table(Prof& prof, hipStream_t s, const PointMap& pm, uint64_t count, felt ninv, felt* out) {
   LAUNCH(prof, "tables", s, (double)count * 16.0,
          hipLaunchKernelGGL(k_l0_table, dim3(blocks_for(count)), dim3(TPB), 0, s, pm, count, ninv, out));
+}
+
+void launch_gu_fill(Prof& prof, hipStream_t s, felt* lde, uint32_t w, uint32_t logn, uint32_t logB, uint32_t j0,
+                    uint32_t logBl, const uint64_t* pos, uint32_t npos, const GuLazy& gl) {
+  const uint64_t cnt = (uint64_t)npos * (w - gl.wi);
+  if (!cnt) return;
+  LAUNCH(prof, "gu_pair", s, (double)cnt * 48.0,
+         hipLaunchKernelGGL(k_gu_fill, dim3(blocks_for(cnt)), dim3(TPB), 0, s, lde, w, logn, logB, j0, logBl, pos, npos,
+                            gl));
 }

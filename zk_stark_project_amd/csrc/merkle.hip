@@ -84,7 +84,18 @@ struct MerkleArgs {
   uint64_t L;       // leaves of this (sub)tree level
   MerkleTail tail;  // k_merkle_fused: finish the tree (+ FRI coin step) in the last block
   LastCol lc;       // k_merkle_leaf2<COLS, true>: column COLS-1 derived from H (zkp_internal.hpp)
+  GuLazy gl;        // MODE 4: LDE rows whose columns >= gl.wi are derived (zkp_internal.hpp)
 };
+
+// value of a lazy GlobalUpdate column c >= gl.wi of the row at base (prev = the
+// previous row of its coset, l = L_0 at the row)
+__device__ __forceinline__ felt gu_lazy_value(const GuLazy& gl, const felt* base, const felt* prev, uint64_t cstride,
+                                              felt l, uint32_t c) {
+  const uint32_t ic = c - gl.d;
+  const felt df = sub(base[ic * cstride], prev[ic * cstride]);
+  const felt kd = gl.smallk ? mul_u32(df, (uint32_t)gl.k.lo) : mul(gl.k, df);
+  return add(kd, mul(gl.cval[ic], l));
+}
 
 // v[COLS-1] = (h - sum_{c<COLS-1} kappa^c v[c]) * kappa^-(COLS-1)  (LastCol; Horner
 // over the known columns: COLS-1 products)
@@ -107,6 +118,14 @@ __device__ __forceinline__ void merkle_leaf(const MerkleArgs& a, uint64_t i, uin
     // natural row i = j + B*t' -> coset j, positions t' + k*R
     const felt* base = a.src + ((i & ((1ull << a.logB) - 1)) * 16) * a.R + (i >> a.logB);
     b3::hash_felts([&](uint32_t k) { return base[k * a.R]; }, a.cols, d);
+  } else if (MODE == 4) {  // MODE 0 with lazy GlobalUpdate columns
+    const uint64_t j = i & ((1ull << a.logB) - 1), t = i >> a.logB;
+    const felt* base = a.src + j * a.n + t;
+    const felt* prev = a.src + j * a.n + (t == 0 ? a.n - 1 : t - 1);
+    const uint64_t cstride = a.n << a.logB;
+    const felt l = a.gl.l0[j * a.n + t];
+    b3::hash_felts([&](uint32_t c) { return c < a.gl.wi ? base[c * cstride] : gu_lazy_value(a.gl, base, prev, cstride, l, c); },
+                   a.cols, d);
   } else if (MODE == 3) {
     // leaf i = j + B*tl sits in chunk k = tl >> logrc, source block j, row tl mod rc
     const uint64_t j = i & ((1ull << a.logB) - 1), tl = i >> a.logB;
@@ -406,7 +425,7 @@ template <int MODE, int COLS = 0, bool DERIVE = false>
 __global__ __launch_bounds__(TPB) void k_leaf_hash_shard(const felt* __restrict__ src, uint64_t n, uint32_t cols,
                                                          uint32_t logBl, uint32_t logrows, uint32_t logrr,
                                                          uint32_t logK, uint32_t k, uint32_t* __restrict__ send,
-                                                         LastCol lc) {
+                                                         LastCol lc, GuLazy gl) {
   const uint64_t q = blockIdx.x * (uint64_t)TPB + threadIdx.x;
   const uint32_t logrc = logrr - logK, logrk = logrows - logK;  // rows per chunk: per destination, in all
   if (q >= (1ull << (logrk + logBl))) return;
@@ -431,6 +450,13 @@ __global__ __launch_bounds__(TPB) void k_leaf_hash_shard(const felt* __restrict_
     const felt* base = src + jl * n + t;
     const uint64_t cstride = n << logBl;
     b3::hash_felts([&](uint32_t c) { return base[c * cstride]; }, cols, d);
+  } else if (MODE == 4) {  // MODE 0 with lazy GlobalUpdate columns
+    const felt* base = src + jl * n + t;
+    const felt* prev = src + jl * n + (t == 0 ? n - 1 : t - 1);
+    const uint64_t cstride = n << logBl;
+    const felt l = gl.l0[jl * n + t];
+    b3::hash_felts([&](uint32_t c) { return c < gl.wi ? base[c * cstride] : gu_lazy_value(gl, base, prev, cstride, l, c); },
+                   cols, d);
   } else {  // FRI row: positions t + k*rows of coset jl (16*rows per coset)
     const felt* base = src + (jl << (logrows + 4)) + t;
     b3::hash_felts([&](uint32_t kk) { return base[kk * rows]; }, cols, d);
@@ -1132,7 +1158,7 @@ bool merkle_upper(Prof& prof, hipStream_t s, uint32_t* nodes, uint64_t L, const 
 }
 
 bool launch_merkle_lde(Prof& prof, hipStream_t s, const felt* lde, uint32_t cols, uint32_t logB, uint64_t n,
-                       uint32_t* nodes, uint64_t L, const MerkleTail* tail, const LastCol* lc) {
+                       uint32_t* nodes, uint64_t L, const MerkleTail* tail, const LastCol* lc, const GuLazy* gl) {
   MerkleArgs a{};
   a.src = lde;
   a.n = n;
@@ -1144,7 +1170,10 @@ bool launch_merkle_lde(Prof& prof, hipStream_t s, const felt* lde, uint32_t cols
   // lane subtrees, whose extra live digests cost waves (kbench_merkle.cpp)
   const uint32_t H = L >= 2 ? 1 : 0;
   static const bool no_preload = getenv("ZKP_NO_LEAF_PRELOAD") != nullptr;  // A/B switch
-  if (lc) {  // the caller checked merkle_can_derive(cols, L)
+  if (gl) {  // lazy GlobalUpdate columns (wide rows: the generic lane pass)
+    a.gl = *gl;
+    merkle_pass<4>(prof, s, a, H, "merkle_lde", (double)L * (gl->wi * 16.0 + 64.0));
+  } else if (lc) {  // the caller checked merkle_can_derive(cols, L)
     if (H != 1 || cols < 2 || cols > 8) abort();
     a.lc = *lc;
     const double bytes = (double)L * (cols * 16.0 + 48.0);
@@ -1302,24 +1331,30 @@ void launch_fri_tail(Prof& prof, hipStream_t s, const FriTailArgs& a) {
 
 void launch_leaf_hash_shard(Prof& prof, hipStream_t s, int mode, const felt* src, uint64_t n, uint32_t cols,
                             uint32_t logBl, uint32_t logrows, uint32_t logrr, uint32_t logK, uint32_t k,
-                            uint32_t* send, const LastCol* lc) {
+                            uint32_t* send, const LastCol* lc, const GuLazy* gl) {
   const uint64_t cnt = 1ull << (logrows - logK + logBl);
   const double bytes = (double)cnt * (cols * 16.0 + 32.0);
   const dim3 g(blocks_for(cnt));
   const LastCol lcv = lc ? *lc : LastCol{};
+  const GuLazy glv = gl ? *gl : GuLazy{};
 #define ZKP_SHARD_LEAF(CC)                                                                                   \
   case CC:                                                                                                   \
     LAUNCH(prof, "leaf_hash_shard", s, bytes,                                                                \
            hipLaunchKernelGGL((k_leaf_hash_shard<0, CC>), g, dim3(TPB), 0, s, src, n, cols, logBl, logrows, \
-                              logrr, logK, k, send, lcv));                                                   \
+                              logrr, logK, k, send, lcv, glv));                                                   \
     break;
 #define ZKP_SHARD_LEAFD(CC)                                                                                  \
   case CC:                                                                                                   \
     LAUNCH(prof, "leaf_hash_shard", s, bytes,                                                                \
            hipLaunchKernelGGL((k_leaf_hash_shard<0, CC, true>), g, dim3(TPB), 0, s, src, n, cols, logBl,    \
-                              logrows, logrr, logK, k, send, lcv));                                          \
+                              logrows, logrr, logK, k, send, lcv, glv));                                          \
     break;
-  if (lc) {  // the caller checked merkle_can_derive
+  if (gl) {  // lazy GlobalUpdate columns
+    if (mode != 0) abort();
+    LAUNCH(prof, "leaf_hash_shard", s, (double)cnt * (gl->wi * 16.0 + 32.0),
+           hipLaunchKernelGGL(k_leaf_hash_shard<4>, g, dim3(TPB), 0, s, src, n, cols, logBl, logrows, logrr, logK, k,
+                              send, lcv, glv));
+  } else if (lc) {  // the caller checked merkle_can_derive
     if (mode != 0 || cols < 2 || cols > 8) abort();
     switch (cols) { ZKP_SHARD_LEAFD(2) ZKP_SHARD_LEAFD(3) ZKP_SHARD_LEAFD(4) ZKP_SHARD_LEAFD(5)
                     ZKP_SHARD_LEAFD(6) ZKP_SHARD_LEAFD(7) ZKP_SHARD_LEAFD(8) }
@@ -1329,11 +1364,11 @@ void launch_leaf_hash_shard(Prof& prof, hipStream_t s, int mode, const felt* src
   } else if (mode == 0)
     LAUNCH(prof, "leaf_hash_shard", s, bytes,
            hipLaunchKernelGGL(k_leaf_hash_shard<0>, g, dim3(TPB), 0, s, src, n, cols, logBl,
-                              logrows, logrr, logK, k, send, lcv));
+                              logrows, logrr, logK, k, send, lcv, glv));
   else
     LAUNCH(prof, "leaf_hash_shard", s, (double)cnt * (cols * 16.0 + 32.0),
            hipLaunchKernelGGL(k_leaf_hash_shard<1>, dim3(blocks_for(cnt)), dim3(TPB), 0, s, src, n, cols, logBl,
-                              logrows, logrr, logK, k, send, lcv));
+                              logrows, logrr, logK, k, send, lcv, glv));
 }
 #undef ZKP_SHARD_LEAFD
 #undef ZKP_SHARD_LEAF

@@ -343,7 +343,8 @@ struct TreeShard {
 // and the function returns true when it did.
 bool commit_rows(zkp_ctx* ctx, zkp_comm* cm, int mode, const felt* src, uint64_t n, uint32_t cols, uint32_t logB,
                  uint32_t logrows, bool sharded, const std::string& name, TreeShard& tr, uint8_t root[32],
-                 bool fetch_root = true, const MerkleTail* coin = nullptr, const LastCol* lc = nullptr) {
+                 bool fetch_root = true, const MerkleTail* coin = nullptr, const LastCol* lc = nullptr,
+                 const GuLazy* gl = nullptr) {
   Prof& pf = ctx->prof;
   hipStream_t st = ctx->stream;
   const uint64_t L = 1ull << (logB + logrows);
@@ -355,7 +356,7 @@ bool commit_rows(zkp_ctx* ctx, zkp_comm* cm, int mode, const felt* src, uint64_t
     if (!ctx->have_cached("merkle_done")) HIP_CHECK(hipMemsetAsync(done, 0, 4, st));
     MerkleTail tail = coin ? *coin : MerkleTail{};
     tail.done = done;
-    bool ran = mode == 0 ? launch_merkle_lde(pf, st, src, cols, logB, n, tr.nodes, L, &tail, lc)
+    bool ran = mode == 0 ? launch_merkle_lde(pf, st, src, cols, logB, n, tr.nodes, L, &tail, lc, gl)
                          : launch_merkle_fri(pf, st, src, 1ull << logrows, logB, 16, tr.nodes, &tail);
     tr.top.assign(2, {});
     if (fetch_root) {  // otherwise the caller reads nodes[1] later
@@ -378,7 +379,8 @@ bool commit_rows(zkp_ctx* ctx, zkp_comm* cm, int mode, const felt* src, uint64_t
   const size_t chunk_words = (size_t)8 << (logBl + logrows - logK), block = (size_t)32 << (logBl + logrr - logK);
   ctx->events(K + 1);
   for (uint32_t k = 0; k < K; k++) {
-    launch_leaf_hash_shard(pf, st, mode, src, n, cols, logBl, logrows, logrr, logK, k, send + k * chunk_words, lc);
+    launch_leaf_hash_shard(pf, st, mode, src, n, cols, logBl, logrows, logrr, logK, k, send + k * chunk_words, lc,
+                           gl);
     HIP_CHECK(hipEventRecord(ctx->up_ev[k], st));
   }
   for (uint32_t k = 0; k < K; k++) {
@@ -1071,6 +1073,8 @@ struct ProofRun {
   felt* gu_cval = nullptr;
   uint32_t* gu_bad = nullptr;    // this rank's check flag (4 words)
   uint32_t* gu_flags = nullptr;  // column-sharded: every rank's flags (all-gathered)
+  bool gu_lazy_on = false;       // the paired LDE columns are derived in the row hash and for the queried rows only
+  GuLazy gu_lazy{};
   const felt* l0_table();
   bool pair_failed();
 
@@ -1200,6 +1204,17 @@ void ProofRun::trace_stage(const zkp_felt* h_trace) {
     gu_cval = ctx->buf<felt>("gu_cval", d);
     gu_bad = ctx->buf<uint32_t>("gu_bad", 4);
     HIP_CHECK(hipMemsetAsync(gu_bad, 0, 16, st));
+    // lazy (device-resident traces): the paired LDE columns are never materialized —
+    // the trace tree's row hash derives them and the openings fill the queried rows
+    // (launch_gu_fill); the coefficient-form constraint evaluation and DEEP never
+    // read the trace LDE (the pointwise A/B switches do, so they keep the columns).
+    // A host trace keeps k_gu_lde: there it runs hidden behind the upload, which
+    // the row hash has to wait for (C3 in A/B, profiles/r03_ab_gu_lazy.txt).
+    static const bool no_lazy = getenv("ZKP_NO_GU_LAZY") || getenv("ZKP_EVAL_POINTWISE") ||
+                                getenv("ZKP_DEEP_POINTWISE");
+    gu_lazy_on = !no_lazy && w >= DEEP_COEF_MIN_W && !h_trace;
+    gu_lazy = GuLazy{gu_cval, l0_table(), air.k, d, R > 1 && cpt && wi < w ? wi : d,
+                     (uint32_t)(air.k.hi == 0 && (air.k.lo >> 32) == 0)};
   }
   if (cpt) {
     // column-sharded interpolation: in round k rank r interpolates
@@ -1254,9 +1269,10 @@ void ProofRun::trace_stage(const zkp_felt* h_trace) {
       const bool slice = (n >> std::min(logn, 11u)) >= R;  // ood_launch splits its blocks
       launch_gu_coef(pf, st, coef, d, logn, air.k, ctx->itws(logN) + ((n >> 1) - 1), i0, np,
                      slice ? (uint64_t)rank * nR : 0, slice ? nR : n, gu_cval);
-      launch_gu_lde(pf, st, tlde, d, logn, logBl, air.k, i0, np, gu_cval, l0_table());
+      if (!gu_lazy_on) launch_gu_lde(pf, st, tlde, d, logn, logBl, air.k, i0, np, gu_cval, l0_table());
     } else {
       paired = false;
+      gu_lazy_on = false;
     }
   } else {
     if (h_trace && R > 1) {
@@ -1338,7 +1354,7 @@ void ProofRun::trace_stage(const zkp_felt* h_trace) {
         const uint32_t i0 = c0 - d;
         launch_gu_check(pf, st, d_trace, d, logn, air.k, i0, cw, 0, logn, gu_cval, gu_bad);
         launch_gu_coef(pf, st, coef, d, logn, air.k, ctx->itws(logN) + ((n >> 1) - 1), i0, cw, 0, n, gu_cval);
-        launch_gu_lde(pf, st, tlde, d, logn, logBl, air.k, i0, cw, gu_cval, l0_table());
+        if (!gu_lazy_on) launch_gu_lde(pf, st, tlde, d, logn, logBl, air.k, i0, cw, gu_cval, l0_table());
         continue;
       }
       NttBatch ib{dcol, coef + (size_t)c0 * n, nullptr, n, n, 1, 1, cw};
@@ -1357,7 +1373,7 @@ void ProofRun::trace_stage(const zkp_felt* h_trace) {
     draw.ncoef = ncoef;
     draw.out = dt_cc;
     coeffs_drawn = commit_rows(ctx, cm, 0, tlde, n, w, logB, logn, R > 1, "ttree", ttree, T.trace_root,
-                               /*fetch_root=*/false, &draw);
+                               /*fetch_root=*/false, &draw, nullptr, gu_lazy_on ? &gu_lazy : nullptr);
   }
   troot_d = R > 1 ? ttree.top_d + 8 : ttree.nodes + 8;  // sharded: the device-built top
   // the composition coefficients (drawn on the device from the trace root)
@@ -1428,7 +1444,15 @@ void ProofRun::constraint_stage() {
       ctx->events(C);
       HIP_CHECK(hipEventRecord(ctx->ev_fork, st));
       HIP_CHECK(hipStreamWaitEvent(ctx->side, ctx->ev_fork, 0));
+      // a derived last column (LastCol) is never extended: only the OOD reads its
+      // coefficients, and a split OOD reads exactly this rank's slice of them
+      const bool ood_split = (n >> std::min(logn, 11u)) >= R;  // ood_launch splits its blocks
       for (uint32_t m = 0; m < C; m++) {
+        if (derive && ood_split && m == C - 1) {
+          HIP_CHECK(hipMemcpyAsync(acoef + (size_t)m * n + p0, slice + (size_t)m * nR, nR * 16,
+                                   hipMemcpyDeviceToDevice, st));
+          break;
+        }
         cm->all_gather(ctx->side, slice + (size_t)m * nR, acoef + (size_t)m * n, nR * 16);
         HIP_CHECK(hipEventRecord(ctx->up_ev[m], ctx->side));
         HIP_CHECK(hipStreamWaitEvent(st, ctx->up_ev[m], 0));
@@ -1651,6 +1675,7 @@ FriCursor ProofRun::fri_layers() {
       }
       full_h.resize(off_w);
       uint32_t* dfull = ctx->buf<uint32_t>("query_full", off_w + 4);
+      if (gu_lazy_on) launch_gu_fill(pf, st, tlde, w, logn, logB, j0, logBl, dpos, o->num_queries, gu_lazy);
       launch_gather_full(pf, st, ga, o->num_queries, dpos, dfull);
       raw_pos.resize(o->num_queries);
       full_d = dfull;
@@ -1799,8 +1824,14 @@ int ProofRun::finish(uint8_t** proof, uint64_t* proof_len, zkp_transcript* tr_ou
   Openings op;
   if (dev_query)
     openings_from_full(raw_pos, pos, full_h.data(), ga, layers, L, F, op);
-  else
+  else {
+    if (gu_lazy_on) {  // the lazy paired columns of the queried rows this rank holds
+      uint64_t* dq = ctx->buf<uint64_t>("gu_fill_pos", np);
+      ctx->upload(dq, pos.data(), np * 8);
+      launch_gu_fill(pf, st, tlde, w, logn, logB, j0, logBl, dq, (uint32_t)np, gu_lazy);
+    }
     gather_openings(ctx, cm, pos, n, logB, j0, tlde, w, ttree, clde, C, ctree, layers, L, F, op);
+  }
   const uint64_t out_words = op.gathered.size();
   // 10. serialize (≙ Proof::to_bytes)
   Writer wr;

@@ -99,8 +99,19 @@ struct LastCol {
   const felt* kap;
   felt* out;
 };
+// GlobalUpdate paired columns that are never materialized: the row hash derives
+// column c >= wi as k*(lde_{c-d}[t] - lde_{c-d}[t-1]) + cval[c-d]*l0[q] (q = the
+// row's index over the source's cosets, t-1 the previous row of its coset; see
+// kernels.hip k_gu_lde), and launch_gu_fill writes them for the queried rows only
+struct GuLazy {
+  const felt* cval;
+  const felt* l0;
+  felt k;
+  uint32_t d, wi, smallk;
+};
 bool launch_merkle_lde(Prof& prof, hipStream_t s, const felt* lde, uint32_t cols, uint32_t logB, uint64_t n,
-                       uint32_t* nodes, uint64_t L, const MerkleTail* tail = nullptr, const LastCol* lc = nullptr);
+                       uint32_t* nodes, uint64_t L, const MerkleTail* tail = nullptr, const LastCol* lc = nullptr,
+                       const GuLazy* gl = nullptr);
 // FRI layer tree over coset-major evaluations (B cosets of 16*m16): leaf r = j + B*t'
 bool launch_merkle_fri(Prof& prof, hipStream_t s, const felt* E, uint64_t m16, uint32_t logB, uint32_t F,
                        uint32_t* nodes, const MerkleTail* tail = nullptr);
@@ -112,7 +123,7 @@ bool merkle_upper(Prof& prof, hipStream_t s, uint32_t* nodes, uint64_t L, const 
 // all-to-all in 2^logK chunks along the destination rows: launch_leaf_hash_shard hashes chunk k
 void launch_leaf_hash_shard(Prof& prof, hipStream_t s, int mode, const felt* src, uint64_t n, uint32_t cols,
                             uint32_t logBl, uint32_t logrows, uint32_t logrr, uint32_t logK, uint32_t k,
-                            uint32_t* send, const LastCol* lc = nullptr);
+                            uint32_t* send, const LastCol* lc = nullptr, const GuLazy* gl = nullptr);
 // sharded tree tops (R <= 64 subtree roots, all-gathered) -> top[1..2R) on the device,
 // then the tail's coin step on the root (tail nullable / MERKLE_TAIL_NONE: none)
 void launch_shard_top(Prof& prof, hipStream_t s, const uint32_t* roots, uint32_t R, uint32_t* top,
@@ -259,6 +270,10 @@ void launch_gu_coef(Prof& prof, hipStream_t s, felt* coef, uint32_t d, uint32_t 
 void launch_gu_lde(Prof& prof, hipStream_t s, felt* lde, uint32_t d, uint32_t logn, uint32_t logBl, felt k,
                    uint32_t c0, uint32_t cw, const felt* cval, const felt* l0);
 void launch_l0_table(Prof& prof, hipStream_t s, const PointMap& pm, uint64_t count, felt ninv, felt* out);
+// the lazy paired columns [wi, w) of the queried rows: pos = natural LDE indices
+// (npos of them), the rows of cosets [j0, j0 + 2^logBl) held here are written
+void launch_gu_fill(Prof& prof, hipStream_t s, felt* lde, uint32_t w, uint32_t logn, uint32_t logB, uint32_t j0,
+                    uint32_t logBl, const uint64_t* pos, uint32_t npos, const GuLazy& gl);
 
 // composition polynomial from CE-coset interpolations (see kernels.hip): for the
 // bit-reversed positions [p0, p0 + nR), n * c_m = (sum_u Si_u * W_u * w_ce^-um) * g^-mn / ce;
