@@ -855,7 +855,7 @@ __global__ __launch_bounds__(TPB) void k_gu_tile_write(const felt* __restrict__ 
 
 // check rows [t0, t0 + 2^logtn) (row 0 excepted) of the column pairs (c0+ci, d+c0+ci),
 // ci < cw, of the natural trace T (column-major); set *bad on any mismatch; c_i
-// when the rows include row 0
+// when the rows include row 0 (cval non-null)
 __global__ __launch_bounds__(TPB) void k_gu_check(const felt* __restrict__ T, uint32_t d, uint32_t logn, felt k,
                                                   uint32_t c0, uint32_t cw, uint64_t t0, uint32_t logtn,
                                                   felt* __restrict__ cval, uint32_t* __restrict__ bad) {
@@ -868,7 +868,7 @@ __global__ __launch_bounds__(TPB) void k_gu_check(const felt* __restrict__ T, ui
   const felt prev = a[t == 0 ? n - 1 : t - 1];
   const felt kd = mul(k, sub(a[t], prev));
   if (t == 0) {
-    cval[i] = sub(b[0], kd);
+    if (cval) cval[i] = sub(b[0], kd);
   } else if (!eq(b[t], kd)) {
     *bad = 1u;
   }

@@ -1074,6 +1074,9 @@ struct ProofRun {
   uint32_t* gu_bad = nullptr;    // this rank's check flag (4 words)
   uint32_t* gu_flags = nullptr;  // column-sharded: every rank's flags (all-gathered)
   bool gu_lazy_on = false;       // the paired LDE columns are derived in the row hash and for the queried rows only
+  bool gu_late_check = false;    // host trace: the paired columns' upload and check still run on the copy stream
+  const zkp_felt* late_h_trace = nullptr;  // host trace whose paired columns late_pairs_upload() still has to send
+  void late_pairs_upload();
   GuLazy gu_lazy{};
   const felt* l0_table();
   bool pair_failed();
@@ -1204,15 +1207,13 @@ void ProofRun::trace_stage(const zkp_felt* h_trace) {
     gu_cval = ctx->buf<felt>("gu_cval", d);
     gu_bad = ctx->buf<uint32_t>("gu_bad", 4);
     HIP_CHECK(hipMemsetAsync(gu_bad, 0, 16, st));
-    // lazy (device-resident traces): the paired LDE columns are never materialized —
-    // the trace tree's row hash derives them and the openings fill the queried rows
-    // (launch_gu_fill); the coefficient-form constraint evaluation and DEEP never
-    // read the trace LDE (the pointwise A/B switches do, so they keep the columns).
-    // A host trace keeps k_gu_lde: there it runs hidden behind the upload, which
-    // the row hash has to wait for (C3 in A/B, profiles/r03_ab_gu_lazy.txt).
+    // lazy: the paired LDE columns are never materialized — the trace tree's row
+    // hash derives them and the openings fill the queried rows (launch_gu_fill);
+    // the coefficient-form constraint evaluation and DEEP never read the trace LDE
+    // (the pointwise A/B switches do, so they keep the columns).
     static const bool no_lazy = getenv("ZKP_NO_GU_LAZY") || getenv("ZKP_EVAL_POINTWISE") ||
                                 getenv("ZKP_DEEP_POINTWISE");
-    gu_lazy_on = !no_lazy && w >= DEEP_COEF_MIN_W && !h_trace;
+    gu_lazy_on = !no_lazy && w >= DEEP_COEF_MIN_W;
     gu_lazy = GuLazy{gu_cval, l0_table(), air.k, d, R > 1 && cpt && wi < w ? wi : d,
                      (uint32_t)(air.k.hi == 0 && (air.k.lo >> 32) == 0)};
   }
@@ -1329,15 +1330,25 @@ void ProofRun::trace_stage(const zkp_felt* h_trace) {
     } else {
       grp.push_back({0u, wd});
     }
-    if (paired) {
-      const uint32_t pw = h_trace ? std::max(1u, d / 10) : d;
-      for (uint32_t c = d; c < w; c += pw) grp.push_back({c, std::min(pw, w - c)});
-    }
+    // paired, device-resident: one group that checks and derives every pair. A host
+    // trace derives from row 0 of the paired columns alone (c_i), so the trace
+    // commitment waits only for columns [0, d): their bulk upload and the check of
+    // rows 1..n-1 follow on the copy stream, behind everything up to the proof's end
+    // (pair_failed joins it)
+    const bool late_pairs = paired && h_trace;
+    if (paired && !h_trace) grp.push_back({d, d});
     const bool piped = h_trace && grp.size() > 1;
+    const size_t G = grp.size();
     if (piped) {  // the copy stream starts after everything already queued
-      ctx->events(grp.size());
+      ctx->events(G + 2);
       HIP_CHECK(hipEventRecord(ctx->ev_fork, st));
       HIP_CHECK(hipStreamWaitEvent(ctx->side, ctx->ev_fork, 0));
+    }
+    if (late_pairs) {  // row 0 of the paired columns first (one 2-D copy of d felts)
+      if (!piped) throw ZkpFail{ZKP_ERR_DEVICE, "paired host trace without column groups"};
+      HIP_CHECK(hipMemcpy2DAsync(const_cast<felt*>(d_trace) + (size_t)d * n, n * 16, h_trace + (size_t)d * n, n * 16,
+                                 16, d, hipMemcpyHostToDevice, ctx->side));
+      HIP_CHECK(hipEventRecord(ctx->up_ev[G], ctx->side));
     }
     for (uint32_t g = 0; g < grp.size(); g++) {
       const uint32_t c0 = grp[g].first, cw = grp[g].second;
@@ -1361,6 +1372,19 @@ void ProofRun::trace_stage(const zkp_felt* h_trace) {
       launch_ntt(pf, st, ib, logn, false, ctx->itws(logN), logN);
       NttBatch lb{coef + (size_t)c0 * n, tlde + (size_t)c0 * Bl * n, Sj0, n, n, Bl, Bl, cw * Bl};
       launch_ntt(pf, st, lb, logn, true, ctx->tws(logN), logN);
+    }
+    if (late_pairs) {
+      // main stream: c_i from row 0, the derived coefficients (and LDE unless lazy)
+      HIP_CHECK(hipStreamWaitEvent(st, ctx->up_ev[G], 0));
+      launch_gu_check(pf, st, d_trace, d, logn, air.k, 0, d, 0, 0, gu_cval, gu_bad);
+      launch_gu_coef(pf, st, coef, d, logn, air.k, ctx->itws(logN) + ((n >> 1) - 1), 0, d, 0, n, gu_cval);
+      if (!gu_lazy_on) launch_gu_lde(pf, st, tlde, d, logn, logBl, air.k, 0, d, gu_cval, l0_table());
+      // copy stream, after the last group's upload: the paired columns and their check,
+      // issued by late_pairs_upload() once the proof's kernels are all queued (a
+      // pageable upload holds the host thread for its whole length)
+      HIP_CHECK(hipEventRecord(ctx->up_ev[G + 1], ctx->side));
+      HIP_CHECK(hipStreamWaitEvent(ctx->copy, ctx->up_ev[G + 1], 0));
+      late_h_trace = h_trace;
     }
   }
   {
@@ -1686,6 +1710,7 @@ FriCursor ProofRun::fri_layers() {
 
 // the proof's host round trip and the replay of the device transcript
 void ProofRun::fri_round_trip(const FriCursor& c) {
+  late_pairs_upload();  // every kernel up to the query tail is queued: the host may block now
   felt* const E = c.E;
   const uint64_t m = c.m, D = c.D;
   const felt off = c.off;
@@ -1878,9 +1903,23 @@ const felt* ProofRun::l0_table() {
   return t;
 }
 
+// host trace, paired: the paired columns [d, w) over PCIe and the check of their rows
+// 1..n-1 on the copy stream (the trace commitment only needed their row 0)
+void ProofRun::late_pairs_upload() {
+  if (!late_h_trace) return;
+  const uint32_t d = w / 2;
+  HIP_CHECK(hipMemcpyAsync(const_cast<felt*>(d_trace) + (size_t)d * n, late_h_trace + (size_t)d * n,
+                           (size_t)d * n * 16, hipMemcpyHostToDevice, ctx->copy));
+  launch_gu_check(pf, ctx->copy, d_trace, d, logn, air.k, 0, d, 0, logn, nullptr, gu_bad);
+  late_h_trace = nullptr;
+  gu_late_check = true;
+}
+
 // a paired trace whose transitions did not hold (one 4-byte read after the proof's last kernels)
 bool ProofRun::pair_failed() {
   if (!paired) return false;
+  late_pairs_upload();  // (a proof whose FRI round trip did not issue it)
+  if (gu_late_check) HIP_CHECK(hipStreamSynchronize(ctx->copy));
   std::vector<uint32_t> f(gu_flags ? 4 * (size_t)R : 4);
   ctx->download(f.data(), gu_flags ? gu_flags : gu_bad, f.size() * 4);
   for (uint32_t v : f)
