@@ -1374,13 +1374,18 @@ void launch_leaf_hash_shard(Prof& prof, hipStream_t s, int mode, const felt* src
 #undef ZKP_SHARD_LEAF
 
 void launch_merkle_from_shards(Prof& prof, hipStream_t s, const uint32_t* recv, uint32_t logB, uint32_t logrr,
-                               uint32_t logK, uint32_t* nodes) {
+                               uint32_t logK, uint32_t* nodes, uint32_t* done) {
+  // with done (a zeroed per-stream counter) the top launch's last block finishes the
+  // subtree instead of a separate one-block launch
+  MerkleTail fin{};
+  fin.done = done;
+  const MerkleTail* tail = done ? &fin : nullptr;
   const uint64_t L = 1ull << (logB + logrr);
   static const bool separate = getenv("ZKP_LEAF_UNPACK") != nullptr;  // A/B switch: the unfused unpack pass
   if (separate || L < 4) {
     LAUNCH(prof, "leaf_unpack", s, (double)L * 64.0,
            hipLaunchKernelGGL(k_leaf_unpack, dim3(blocks_for(L)), dim3(TPB), 0, s, recv, logB, logrr, logK, nodes, L));
-    merkle_upper(prof, s, nodes, L, nullptr);
+    merkle_upper(prof, s, nodes, L, tail);
     return;
   }
   // the unpack fused into the first 2-level lane pass: each lane loads its 4 leaf
@@ -1392,7 +1397,7 @@ void launch_merkle_from_shards(Prof& prof, hipStream_t s, const uint32_t* recv, 
   a.nodes = nodes;
   a.L = L;
   merkle_pass<3>(prof, s, a, 2, "merkle_upper", (double)L * 32.0 * 2.5);
-  merkle_upper(prof, s, nodes, L >> 2, nullptr);
+  merkle_upper(prof, s, nodes, L >> 2, tail);
 }
 
 // top levels of a sharded tree from the all-gathered subtree roots (R <= 64):

@@ -390,7 +390,9 @@ bool commit_rows(zkp_ctx* ctx, zkp_comm* cm, int mode, const felt* src, uint64_t
   HIP_CHECK(hipEventRecord(ctx->up_ev[K], ctx->side));
   HIP_CHECK(hipStreamWaitEvent(st, ctx->up_ev[K], 0));
   tr.nodes = ctx->buf<uint32_t>(name, (size_t)16 * tr.Lr);
-  launch_merkle_from_shards(pf, st, recv, logB, logrr, logK, tr.nodes);
+  uint32_t* done = ctx->buf<uint32_t>("merkle_done", 1);
+  if (!ctx->have_cached("merkle_done")) HIP_CHECK(hipMemsetAsync(done, 0, 4, st));
+  launch_merkle_from_shards(pf, st, recv, logB, logrr, logK, tr.nodes, done);
   // the top levels on the device from the all-gathered subtree roots: the coin
   // kernels read the root there, and the host fetches tr.top with the transcript
   // (fetch_root = false) instead of a round trip per commitment

@@ -129,7 +129,7 @@ void launch_leaf_hash_shard(Prof& prof, hipStream_t s, int mode, const felt* src
 void launch_shard_top(Prof& prof, hipStream_t s, const uint32_t* roots, uint32_t R, uint32_t* top,
                       const MerkleTail* tail);
 void launch_merkle_from_shards(Prof& prof, hipStream_t s, const uint32_t* recv, uint32_t logB, uint32_t logrr,
-                               uint32_t logK, uint32_t* nodes);
+                               uint32_t logK, uint32_t* nodes, uint32_t* done = nullptr);
 // internal nodes nodes[1..L) from leaves nodes[L..2L)
 void launch_merkle_tree(Prof& prof, hipStream_t s, uint32_t* nodes, uint64_t L);
 constexpr uint32_t PACK_MAX = 16;
