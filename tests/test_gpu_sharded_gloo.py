@@ -30,8 +30,10 @@ def _case(kind):
         p, trace = mimc_case(1 << 12, opts)
         return AIR_MIMC, trace, p.get_pub_inputs(trace).to_elements(), opts
     opts = ProofOptions.reference()
-    p = gu_prover(16, 1 << 11, opts, seed=21)
+    p = gu_prover(16, 1 << 13, opts, seed=21)
     trace = p.build_trace()
+    if kind == "global_update_dev_bad":  # a failed transition on rank 1's rows: both ranks fall back, unpaired
+        trace.data[70, (1 << 12) + 9, 0] ^= 0x77
     return AIR_GLOBAL_UPDATE, trace, p.get_pub_inputs(trace).to_elements(), opts
 
 
@@ -53,7 +55,14 @@ def _rank(rank, world, port, kind, q, fail_rank):
             dist.destroy_process_group()
             return
         try:
-            data, _ = ctx.prove_sharded(comm, air, trace.data, pub, opts)
+            if kind.startswith("global_update_dev"):  # device-resident: the paired path, flags over gloo
+                w, n = trace.data.shape[0], trace.data.shape[1]
+                d = ctx.alloc(trace.data.nbytes)
+                ctx.to_device(d, trace.data)
+                data, _ = ctx.prove_sharded(comm, air, d, pub, opts, shape=(w, n))
+                ctx.free(d)
+            else:
+                data, _ = ctx.prove_sharded(comm, air, trace.data, pub, opts)
             q.put((rank, "ok", data))
         except Exception as e:  # noqa: BLE001
             q.put((rank, "error", repr(e)))
@@ -85,7 +94,7 @@ def run_group(kind, world=2, fail_rank=-1, timeout=240):
     return res
 
 
-@pytest.mark.parametrize("kind", ["mimc", "mimc_b16", "global_update"])
+@pytest.mark.parametrize("kind", ["mimc", "mimc_b16", "global_update", "global_update_dev", "global_update_dev_bad"])
 def test_two_process_gloo_sharded_equals_single(ctx, kind):
     air, trace, pub, opts = _case(kind)
     single, _ = ctx.prove(air, trace.data, pub, opts)
