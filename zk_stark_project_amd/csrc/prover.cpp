@@ -1226,7 +1226,8 @@ void ProofRun::trace_stage(const zkp_felt* h_trace) {
     // columns in order at coef + k*R*cpr*n while the main stream extends round
     // k - 1's columns on this rank's cosets. Nothing but coefficients crosses xGMI.
     // rounds: the most that divide cpt, up to 6 — only round 0's exchange is
-    // exposed (C5 at R = 8: 5 rounds of 3 columns per rank, 24 columns per LDE)
+    // exposed (C5 at R = 8: 4 rounds of 2 of the 64 paired-trace columns per rank,
+    // 16 columns per LDE; unpaired 5 rounds of 3)
     uint32_t K = 6;
     while (cpt % K) K--;
     const uint32_t cpr = cpt / K;
@@ -1298,26 +1299,13 @@ void ProofRun::trace_stage(const zkp_felt* h_trace) {
       }
       h_trace = nullptr;  // resident on every rank from here
     }
-    // column groups: one for device-resident traces. Host traces upload group g+1
-    // on the copy stream while the main stream interpolates and extends group g;
-    // the groups grow geometrically (x1.5 from ~w/40 columns: C3 3, 4, 6, ..., 38),
-    // so only the small first group's upload is exposed and every later one hides
-    // behind the previous group's LDE (a column's upload takes ~0.55x its LDE at C3)
-    // GlobalUpdate column pairing (k_gu_check): only columns [0, d)
-    // are interpolated and extended; column d+i is checked against its transition
-    // constraint and derived from column i in the same group (its upload rides
-    // with column i's). A trace that fails the check is proven again unpaired
-    // (prove_impl), so the result never depends on the shortcut.
     const uint32_t wd = paired ? d : w;  // columns interpolated and extended here
-    // groups (first column, columns): one for device-resident traces. Host traces
-    // upload group g+1 on the copy stream while the main stream works on group g.
-    // Columns [0, d): interpolation + coset LDE, the groups growing geometrically
-    // (x1.5 from ~w/40 columns: C3 unpaired 3, 4, 6, ..., 38), so only the small
-    // first group's upload is exposed and every later one hides behind the previous
-    // group's LDE (a column uploads in ~0.55x its LDE at C3). Paired columns
-    // [d, w) follow in equal groups of ~d/10: their derivation is ~5x cheaper than
-    // an LDE, so the upload is the critical path there and a small last group
-    // leaves little after it.
+    // groups (first column, columns) of [0, wd): one for device-resident traces.
+    // Host traces upload group g+1 on the side stream while the main stream
+    // interpolates and extends group g; the groups grow geometrically (x1.5 from
+    // ~w/40 columns: C3 unpaired 3, 4, 6, ..., 38), so only the small first group's
+    // upload is exposed and every later one hides behind the previous group's LDE
+    // (a column uploads in ~0.55x its LDE at C3).
     std::vector<std::pair<uint32_t, uint32_t>> grp;
     static const uint32_t growth =  // percent (A/B switch ZKP_UPLOAD_GROWTH)
         getenv("ZKP_UPLOAD_GROWTH") ? std::max(110, atoi(getenv("ZKP_UPLOAD_GROWTH"))) : 150u;
@@ -1334,9 +1322,9 @@ void ProofRun::trace_stage(const zkp_felt* h_trace) {
     }
     // paired, device-resident: one group that checks and derives every pair. A host
     // trace derives from row 0 of the paired columns alone (c_i), so the trace
-    // commitment waits only for columns [0, d): their bulk upload and the check of
-    // rows 1..n-1 follow on the copy stream, behind everything up to the proof's end
-    // (pair_failed joins it)
+    // commitment waits only for columns [0, d): the paired columns' bulk upload and
+    // the check of their rows 1..n-1 follow on the copy stream once the proof's
+    // kernels are queued (late_pairs_upload; pair_failed joins it)
     const bool late_pairs = paired && h_trace;
     if (paired && !h_trace) grp.push_back({d, d});
     const bool piped = h_trace && grp.size() > 1;
