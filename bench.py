@@ -53,11 +53,16 @@ KERNEL_SYMBOL = {
     "merkle_lde": ("void k_merkle_lane<0,", "void k_merkle_leaf2<"), "eval_mimc": "k_eval_mimc",
     "eval_linear": ("void k_eval_linear<", "void k_eval_linear_pts<"),
 }
-# launch name -> SURVEY.md Appendix C stages whose algorithmic bytes that kernel moves
+# launch name -> SURVEY.md Appendix C stages whose algorithmic bytes that kernel moves.
+# ntt_dit is charged per column it actually extends (kernel_stage_bytes): the trace
+# columns that are interpolated and extended (GlobalUpdate pairing derives the other
+# half) and the composition columns (the derived last column, LastCol, is written by
+# the leaf pass, not by an NTT)
 KERNEL_STAGES = {
     "ntt_dit": ("lde", "comp_lde"), "ntt_dif": ("intt", "comp_intt"), "deep": ("deep",),
     "eval_mimc": ("eval",), "eval_linear": ("eval",),
 }
+UBENCH_BFLY = "profiles/r04_ubench_bfly.json"  # tests/native/ubench_bfly.hip on the box: the butterfly floor
 PMC_TAGS = ("r03", "r02_final", "r02", "r01")  # newest committed PMC summaries first (scripts/profile_round.sh)
 
 
@@ -82,6 +87,46 @@ def stage_bytes(w: int, n: int, B: int, ce: int, C: int, rem: int = 7, F: int = 
         D //= F
     s["fri"] = fri
     return s
+
+
+def lde_columns(wl: dict, R: int) -> tuple:
+    """(trace columns, composition columns) that ntt_dit's launches extend per proof."""
+    w, C, ce, B = wl["width"], wl["C"], wl["ce"], wl["opts"].blowup_factor
+    comp = C - 1 if (ce == B and 2 <= C <= 8) else C  # LastCol: derived in the composition leaf pass
+    trace = w
+    if wl.get("paired"):  # GlobalUpdate: columns 0..59 (rounded up to a multiple of the ranks) are extended
+        d = w // 2
+        trace = d if R == 1 else -(-d // R) * R
+    return trace, comp
+
+
+def kernel_stage_bytes(kernel: str, sb: dict, wl: dict, R: int):
+    """Appendix C bytes per proof that `kernel` is charged with, and a source note."""
+    stages = KERNEL_STAGES.get(kernel)
+    if not stages:
+        return None, None
+    if kernel != "ntt_dit":
+        return sum(sb[s] for s in stages), f"stages {'+'.join(stages)}"
+    n, N = wl["n"], wl["n"] * wl["opts"].blowup_factor
+    tcols, ccols = lde_columns(wl, R)
+    per_col = n * E + N * E  # Appendix C lde / comp_lde per column
+    return ((tcols + ccols) * per_col,
+            f"stages lde+comp_lde for the columns ntt_dit extends: {tcols} trace + {ccols} composition column(s) "
+            f"x (nE + NE) (of w = {wl['width']}, C = {wl['C']})")
+
+
+def floor_rate():
+    """G butterflies/s of the committed butterfly micro-benchmark, or None."""
+    path = os.path.join(ROOT, UBENCH_BFLY)
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        return json.load(f).get("gbfly_per_s")
+
+
+def zkp_env() -> dict:
+    """Every ZKP_* switch set in this process's environment (A/B switches of the library)."""
+    return {k: v for k, v in sorted(os.environ.items()) if k.startswith("ZKP_")}
 
 
 def load_pmc(kind: str, air: str, kernel: str):
@@ -240,6 +285,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--no-sharded-leg", action="store_true", help="N>1 replicas: skip the C4 sharded proof")
+    ap.add_argument("--sharded-leg", action="store_true",
+                    help="run the C4 sharded leg at N = 1 too (a world-1 RCCL rehearsal of its collectives and checks)")
     ap.add_argument("--stats", action="store_true", help="print the per-kernel table to stderr")
     ap.add_argument("--air", choices=["mimc", "agg"], default="mimc",
                     help="mimc = C2 (default, the BASELINE metric); agg = C3 GlobalUpdate (64 updates, 2^18 rows)")
@@ -257,7 +304,7 @@ def make_workload(air: str, sharded: bool, log_n, blowup: int, seed_rank: int, c
         trace = prover.build_trace(42 * 10**6 + seed_rank, n)  # independent trace per replica
         cfg = "BASELINE configs[3], domain-sharded" if sharded else "BASELINE configs[1]"
         return dict(air_id=AIR_MIMC, width=1, n=n, log_n=log_n, opts=opts, trace=trace, prover=prover, ce=8, C=6,
-                    workload=f"MiMC AIR 2^{log_n}-step trace, blowup={blowup} ({cfg})")
+                    paired=False, workload=f"MiMC AIR 2^{log_n}-step trace, blowup={blowup} ({cfg})")
     import random
     log_n = log_n or (20 if sharded else 18)
     n = 1 << log_n
@@ -272,7 +319,7 @@ def make_workload(air: str, sharded: bool, log_n, blowup: int, seed_rank: int, c
     trace = prover.build_trace()
     cfg = "BASELINE configs[4], domain-sharded" if sharded else "BASELINE configs[2]"
     return dict(air_id=AIR_GLOBAL_UPDATE, width=120, n=n, log_n=log_n, opts=opts, trace=trace, prover=prover,
-                ce=2, C=1, workload=f"GlobalUpdate AIR, {ndev} updates padded to 2^{log_n} rows, w=120 ({cfg})")
+                ce=2, C=1, paired=True, workload=f"GlobalUpdate AIR, {ndev} updates padded to 2^{log_n} rows, w=120 ({cfg})")
 
 
 WATCHDOG_EXIT = 3  # exit status of every rank when the sharded leg hangs
@@ -321,14 +368,41 @@ def sharded_leg(ctx, rank: int, world: int, dist, local_rank: int, on_timeout=No
             return ctx.prove_sharded(comm, wl["air_id"], wl["trace"].data, pub, wl["opts"])
         elapsed, _, (proof, _) = timed_replicas(once, steps, 2, dist=dist, device_sync=torch.cuda.synchronize,
                                                 device=f"cuda:{local_rank}")
+        check = sharded_self_check(ctx, wl, pub, proof, rank, world, dist, local_rank)
     finally:
         comm.close()
     done.set()
     return {"metric": "STARK proofs/sec + prove-time ms, MiMC AIR 2^22-step trace, one proof domain-sharded over "
                       "all GPUs", "workload": wl["workload"], "value": round(steps / elapsed, 3), "unit": "proofs/s",
             "ms_per_proof": round(elapsed / steps * 1e3, 3), "steps": steps, "warmup": 2, "scaling": "strong",
-            "parallelism": f"coset-sharded{world} (RCCL)", "proof_bytes": len(proof), "fabric": fabric,
+            "parallelism": f"coset-sharded{world} (RCCL)", "proof_bytes": len(proof), "fabric": fabric, **check,
             "bytes_per_proof_8d": sum(stage_bytes(1, 1 << 22, 8, 8, 6).values())}
+
+
+def sharded_self_check(ctx, wl, pub, proof, rank: int, world: int, dist, local_rank: int) -> dict:
+    """After the timed sharded proofs (outside the timed region): every rank checks its
+    last proof with the product verifier (zkp_verify) and hashes its bytes; rank 0 also
+    proves the same trace on its one GPU (zkp_prove) and compares. The flags and
+    hashes are all-gathered, so the line says whether every rank's RCCL proof is the
+    world-1 proof, byte for byte."""
+    import hashlib
+    import torch
+    from zk_stark_project_amd._native import verify_status
+    ok = verify_status(wl["air_id"], proof, pub, wl["opts"]) == 0
+    exact = True
+    if rank == 0:
+        ref, _ = ctx.prove(wl["air_id"], wl["trace"].data, pub, wl["opts"])
+        exact = ref == proof
+    h = int.from_bytes(hashlib.blake2b(proof, digest_size=7).digest(), "little")
+    mine = torch.tensor([h, int(ok), int(exact)], dtype=torch.int64, device=f"cuda:{local_rank}")
+    allv = [torch.zeros_like(mine) for _ in range(world)]
+    dist.all_gather(allv, mine)
+    rows = [t.tolist() for t in allv]
+    same = all(r[0] == rows[0][0] for r in rows)
+    return {"verified": all(r[1] for r in rows), "bit_exact_vs_world1": bool(rows[0][2]) and same,
+            "ranks_identical": same,
+            "self_check": "zkp_verify on every rank; rank 0's world-1 zkp_prove of the same trace vs the sharded "
+                          "bytes; every rank's proof hash all-gathered"}
 
 
 def main():
@@ -337,11 +411,14 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
-    if world > 1:
+    if world > 1 or args.sharded_leg:
         import torch
         import torch.distributed as tdist
         torch.cuda.set_device(local_rank)
-        tdist.init_process_group("nccl")
+        if world > 1:
+            tdist.init_process_group("nccl")
+        else:  # world-1 rehearsal outside torchrun
+            tdist.init_process_group("nccl", init_method="tcp://127.0.0.1:29533", rank=0, world_size=1)
         dist = tdist
 
     def cuda_sync():
@@ -430,7 +507,7 @@ def main():
 
     if comm is not None:
         comm.close()
-    run_sharded = world > 1 and not sharded and not args.no_sharded_leg
+    run_sharded = (world > 1 or args.sharded_leg) and not sharded and not args.no_sharded_leg
     if rank != 0:
         failed = False
         if run_sharded:  # collective with rank 0's leg below
@@ -455,8 +532,19 @@ def main():
     dom = stats[dom_name]  # HIP events of the timed region
     dom_avg_ms = dom["ms"] / dom["launches"]
     launches_per_proof = dom["launches"] / args.steps
-    stages = KERNEL_STAGES.get(dom_name)
-    alg = sum(sb[s] for s in stages) / R / launches_per_proof if stages else None
+    kbytes, ksrc = kernel_stage_bytes(dom_name, sb, wl, R)
+    alg = kbytes / R / launches_per_proof if kbytes else None
+    # the NTT's butterfly floor: butterflies of the extended columns' coset NTTs at the
+    # micro-benchmark's register-resident rate, against the kernel's time per proof
+    valu_floor = None
+    if dom_name == "ntt_dit" and floor_rate():
+        tcols, ccols = lde_columns(wl, R)
+        bfly = (tcols + ccols) * B / R * (n // 2) * wl["log_n"]
+        kernel_ms = dom_avg_ms * launches_per_proof
+        floor_ms = bfly / (floor_rate() * 1e9) * 1e3
+        valu_floor = {"butterflies_per_proof": bfly, "floor_gbfly_per_s": floor_rate(), "floor_ms": round(floor_ms, 4),
+                      "kernel_ms_per_proof": round(kernel_ms, 4), "valu_floor_frac": round(floor_ms / kernel_ms, 3),
+                      "source": f"{UBENCH_BFLY} (tests/native/ubench_bfly.hip, the library's butterfly forms)"}
     traffic, traffic_src = pmc_traffic(dom_name, args.air, args.mode)
     ms = elapsed / args.steps * 1e3
     roofline = {
@@ -469,9 +557,8 @@ def main():
         "traffic": traffic,
         "traffic_source": traffic_src,
         "algorithmic_bytes_per_launch": alg,
-        "algorithmic_bytes_source": (f"SURVEY.md §8(d)/Appendix C stages {'+'.join(stages)} = "
-                                     f"{sum(sb[s] for s in stages)} B per proof / {launches_per_proof:g} launches"
-                                     if stages else None),
+        "algorithmic_bytes_source": (f"SURVEY.md §8(d)/Appendix C {ksrc} = {kbytes} B per proof / "
+                                     f"{launches_per_proof:g} launches" if kbytes else None),
         "traffic_over_algorithmic": round(traffic / alg, 2) if traffic and alg else None,
         "traffic_model_per_launch": dom["bytes"] / dom["launches"],
         "avg_launch_ms": round(dom_avg_ms, 5),
@@ -480,6 +567,8 @@ def main():
         "whole_proof_frac": round(bytes_per_proof / R / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
         "bytes_per_proof_8d": bytes_per_proof,
         "valu": valu_side(dom_name, args.air, args.mode),
+        "valu_floor_frac": valu_floor["valu_floor_frac"] if valu_floor else None,
+        "valu_floor": valu_floor,
     }
 
     cpu = None
@@ -536,6 +625,7 @@ def main():
                    "trace_length": n, "trace_width": width, "blowup": B, "num_queries": 40, "grinding": 21,
                    "fri_folding": 16, "fri_remainder_max_degree": 7,
                    "parallelism": f"coset-sharded{world} (RCCL)" if sharded else f"replicas{world}",
+                   "env": zkp_env(),
                    "step": ("GlobalUpdate trace built on each rank's device from the updates + zkp_prove_sharded"
                             if sharded and args.air == "agg" else
                             "zkp_prove: host trace (pageable) -> proof bytes, PCIe upload included")},

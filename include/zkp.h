@@ -81,7 +81,7 @@ typedef enum zkp_status {
   ZKP_OK = 0,
   ZKP_ERR_INVALID_OPTIONS = 1,
   ZKP_ERR_UNSUPPORTED_FIELD_EXTENSION = 2,
-  ZKP_ERR_TRACE_SHAPE = 3,   /* n < 8, n not a power of two, width 0 or > 255, n*blowup too big */
+  ZKP_ERR_TRACE_SHAPE = 3,   /* n < 8, n not a power of two, width 0 or > 255, n > 2^23, n*blowup > 2^28 */
   ZKP_ERR_PUB_INPUTS = 4,    /* wrong number of public input elements / inconsistent values */
   ZKP_ERR_DEVICE = 5,        /* HIP failure or no device */
   ZKP_ERR_NONCE = 6,         /* grinding nonce not found */

@@ -151,6 +151,68 @@ def test_global_update_pairing_edge_traces(ctx, edit, device):
     assert ok == (edit == "row0")
 
 
+@pytest.mark.parametrize("edit", ["transition", "last_row", "wrong_result", "wrong_start"])
+@pytest.mark.parametrize("device", [False, True])
+def test_mimc_invalid_trace_lastcol(ctx, edit, device):
+    """The derived last composition column (LastCol, MiMC at blowup 8: ce = B) equals
+    winterfell's column only when the segments CompositionPoly::new drops are zero,
+    i.e. for a trace that satisfies its constraints. A broken transition, a broken
+    last row or a wrong boundary value makes them nonzero: k_comp_dft raises the flag
+    and the proof is made again with the column extended. Bytes = the oracle's (which
+    proves whatever it is given); the verifier rejects the proof."""
+    opts = ProofOptions(40, 8, 8)
+    n = 1024
+    p, trace = mimc_case(n, opts)
+    pub_el = list(p.get_pub_inputs(trace).to_elements())
+    data = np.array(trace.data, copy=True)
+    if edit == "transition":
+        data[0, 5, 0] ^= np.uint64(0x5A5A)
+    elif edit == "last_row":
+        data[0, n - 1, 0] ^= np.uint64(0x5A5A)
+    elif edit == "wrong_result":
+        pub_el[1] = (pub_el[1] + 1) % P
+    else:
+        pub_el[0] = (pub_el[0] + 7) % P
+    if device:
+        d = ctx.alloc(data.nbytes)
+        try:
+            ctx.to_device(d, data)
+            gpu, gtr = ctx.prove_device(AIR_MIMC, d, 1, n, pub_el, opts)
+        finally:
+            ctx.free(d)
+    else:
+        gpu, gtr = ctx.prove(AIR_MIMC, data, pub_el, opts)
+    ref, otr = O.prove(AIR_MIMC, data.tobytes(), 1, n, to_bytes(pub_el), opts)
+    assert bytes(gtr.constraint_root) == bytes(otr.constraint_root)
+    assert gpu == ref
+    assert O.verify(AIR_MIMC, gpu, to_bytes(pub_el), opts) != 0
+
+
+def test_shape_limits_return_status(ctx):
+    """Shapes past the kernels' 32-bit offsets (n * blowup > 2^28) or the OOD block
+    tree (n > 2^23) are refused with ZKP_ERR_TRACE_SHAPE (3) before any launch; the
+    process survives and the context stays usable."""
+    from zk_stark_project_amd._native import ZkpError
+    n = 1 << 23
+    big = np.zeros((1, n, 2), dtype=np.uint64)
+    with pytest.raises(ZkpError) as e:
+        ctx.prove(AIR_MIMC, big, [0, 0], ProofOptions(40, 64, 0))
+    assert e.value.code == 3
+    del big
+    with pytest.raises(ZkpError) as e:
+        ctx.trace_lde_commit(np.zeros((1, 1 << 22, 2), dtype=np.uint64), 128, want_lde=False)
+    assert e.value.code == 3
+    with pytest.raises(ZkpError) as e:
+        ctx.prove(AIR_MIMC, np.zeros((1, 1 << 24, 2), dtype=np.uint64), [0, 0], ProofOptions(40, 8, 0))
+    assert e.value.code == 3
+    # still usable
+    opts = ProofOptions(40, 8, 4)
+    p, trace = mimc_case(256, opts)
+    pub_el = p.get_pub_inputs(trace).to_elements()
+    gpu, _ = ctx.prove(AIR_MIMC, trace.data, pub_el, opts)
+    assert O.verify(AIR_MIMC, gpu, to_bytes(pub_el), opts) == 0
+
+
 # ---------------------------------------------------------------- full-size configs
 @pytest.mark.slow
 def test_mimc_c2_full_size_bit_exact(ctx):

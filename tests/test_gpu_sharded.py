@@ -52,6 +52,27 @@ def test_mimc_sharded_matches_oracle(rank_ctxs):
     assert O.verify(AIR_MIMC, res[0][0], to_bytes(pub), opts) == 0
 
 
+@pytest.mark.parametrize("world", [2, 8])
+@pytest.mark.parametrize("edit", ["transition", "wrong_result"])
+def test_mimc_sharded_invalid_trace_lastcol(rank_ctxs, world, edit):
+    """A MiMC trace that breaks its constraints, proven over R ranks: every rank's
+    dropped-segment check is all-gathered and all ranks prove again with the last
+    composition column extended. Bytes = the oracle's."""
+    n = 1 << 12
+    opts = ProofOptions(40, 8, 8)
+    p, trace = mimc_case(n, opts)
+    pub = list(p.get_pub_inputs(trace).to_elements())
+    data = np.array(trace.data, copy=True)
+    if edit == "transition":
+        data[0, n // 2 + 9, 0] ^= np.uint64(0x77)  # a row of rank 1's slice at world 2
+    else:
+        pub[1] = (pub[1] + 1) % (2**128 - 45 * 2**40 + 1)
+    res = prove_local_group(world, AIR_MIMC, data, pub, opts, contexts=rank_ctxs[:world])
+    ref, _ = O.prove(AIR_MIMC, data.tobytes(), 1, n, to_bytes(pub), opts)
+    check_all_equal(res, ref)
+    assert O.verify(AIR_MIMC, ref, to_bytes(pub), opts) != 0
+
+
 @pytest.mark.parametrize("world", [2, 4, 8])
 @pytest.mark.parametrize("n,edit", [(1 << 11, None), (1 << 13, None), (1 << 13, "transition"), (1 << 11, "row0")])
 def test_global_update_sharded_device_paired(ctx, rank_ctxs, world, n, edit):

@@ -83,19 +83,39 @@ struct LocalComm : zkp_comm {
 };
 
 // ------------------------------------------------------------------ RCCL
+// Ordering invariant: every collective of a communicator runs on
+// the communicator's own stream `cs`, in the order the prover issues them (the
+// same program order on every rank). The caller's stream (main, side or copy)
+// hands over with an event before the collective and waits for one after it, so
+// collectives issued from different prover streams are never in flight on one
+// communicator at the same time, whatever RCCL does internally with streams.
 struct RcclComm : zkp_comm {
   ncclComm_t c = nullptr;
+  hipStream_t cs = nullptr;
+  hipEvent_t ev_in = nullptr, ev_out = nullptr;
   const char* kind() const override { return "rccl"; }
+  void enter(hipStream_t st) {
+    hip_ok(hipEventRecord(ev_in, st), "rccl: record on the caller stream");
+    hip_ok(hipStreamWaitEvent(cs, ev_in, 0), "rccl: comm stream waits");
+  }
+  void leave(hipStream_t st) {
+    hip_ok(hipEventRecord(ev_out, cs), "rccl: record on the comm stream");
+    hip_ok(hipStreamWaitEvent(st, ev_out, 0), "rccl: caller stream waits");
+  }
   void all_to_all(hipStream_t st, const void* send, void* recv, size_t b) override {
+    enter(st);
     nccl_ok(ncclGroupStart(), "ncclGroupStart");
     for (int s = 0; s < world; s++) {
-      nccl_ok(ncclSend(static_cast<const char*>(send) + (size_t)s * b, b, ncclUint8, s, c, st), "ncclSend");
-      nccl_ok(ncclRecv(static_cast<char*>(recv) + (size_t)s * b, b, ncclUint8, s, c, st), "ncclRecv");
+      nccl_ok(ncclSend(static_cast<const char*>(send) + (size_t)s * b, b, ncclUint8, s, c, cs), "ncclSend");
+      nccl_ok(ncclRecv(static_cast<char*>(recv) + (size_t)s * b, b, ncclUint8, s, c, cs), "ncclRecv");
     }
     nccl_ok(ncclGroupEnd(), "ncclGroupEnd");
+    leave(st);
   }
   void all_gather(hipStream_t st, const void* send, void* recv, size_t b) override {
-    nccl_ok(ncclAllGather(send, recv, b, ncclUint8, c, st), "ncclAllGather");
+    enter(st);
+    nccl_ok(ncclAllGather(send, recv, b, ncclUint8, c, cs), "ncclAllGather");
+    leave(st);
   }
   void abort() override {
     if (c) (void)ncclCommAbort(c);
@@ -103,6 +123,10 @@ struct RcclComm : zkp_comm {
   }
   ~RcclComm() override {
     if (c) (void)ncclCommDestroy(c);
+    if (cs) (void)hipStreamSynchronize(cs);
+    if (ev_in) (void)hipEventDestroy(ev_in);
+    if (ev_out) (void)hipEventDestroy(ev_out);
+    if (cs) (void)hipStreamDestroy(cs);
   }
 };
 
@@ -184,6 +208,12 @@ zkp_comm* make_rccl_comm(int device, const unsigned char id[128], int world, int
   auto* c = new RcclComm();
   c->rank = rank;
   c->world = world;
+  if (hipStreamCreateWithFlags(&c->cs, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_in, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_out, hipEventDisableTiming) != hipSuccess) {
+    delete c;
+    throw CommError("rccl: stream/event creation failed");
+  }
   ncclResult_t r = ncclCommInitRank(&c->c, world, u, rank);
   if (r != ncclSuccess) {
     delete c;

@@ -11,13 +11,7 @@
 #include <stdint.h>
 // included from felt.hpp inside the device compilation pass only
 
-// ZKP_ASM_VOLATILE (tuning experiment): volatile asm keeps the source order of
-// the carry chains (the interleaving below) instead of the machine scheduler's
-#ifdef ZKP_ASM_VOLATILE
-#define ZKP_ASM asm volatile
-#else
 #define ZKP_ASM asm
-#endif
 
 namespace fpd {
 
@@ -149,6 +143,32 @@ __device__ __forceinline__ felt canon_from(uint32_t s0, uint32_t s1, uint32_t s2
   return join(sel(s0, t0, m), sel(s1, t1, m), sel(s2, t2, m), sel(s3, t3, m));
 }
 
+// Fast canonical forms. A 128-bit value z (plus a carry bit k past 2^128) with
+// k = 0 and z3 != 0xffffffff is below 2^128 - 2^96 < p, so already canonical; a
+// random z misses that with probability 2^-32 per lane. The check is one v_cmp
+// whose wave ballot, OR'd with k, is uniform (SGPR masks), so `rare` is a scalar
+// branch: a wave runs the exact select (canon_from) only when one of its lanes
+// needs it, and the result is the same field element either way.
+__device__ __forceinline__ felt canon_rare(uint32_t z0, uint32_t z1, uint32_t z2, uint32_t z3, uint64_t k) {
+  const uint64_t rare = k | __builtin_amdgcn_ballot_w64(z3 == 0xffffffffu);
+  if (rare) return canon_from(z0, z1, z2, z3, k);
+  return join(z0, z1, z2, z3);
+}
+
+// a + b for canonical a, b: the sum S < 2p. Carry c set: S - p = s + C, which is
+// < p. Carry clear: s is S, canonical unless s >= p (then s3 = 0xffffffff: the
+// rare branch takes the exact select).
+__device__ __forceinline__ felt add_sum(uint32_t s0, uint32_t s1, uint32_t s2, uint32_t s3, uint64_t c) {
+  if (__builtin_amdgcn_ballot_w64(s3 == 0xffffffffu)) return canon_from(s0, s1, s2, s3, c);
+  const uint32_t m0 = sel_0_m1(c), m1 = m0 & C1;  // c ? C : 0
+  uint64_t g;
+  const uint32_t t0 = add_co(s0, m0, g);
+  const uint32_t t1 = addc_co(s1, m1, g, g);
+  const uint32_t t2 = addc_co_0(s2, g, g);
+  const uint32_t t3 = addc_0(s3, g);
+  return join(t0, t1, t2, t3);
+}
+
 __device__ __forceinline__ felt add(felt a, felt b) {
   L4 x = split(a), y = split(b);
   uint64_t c;
@@ -156,7 +176,7 @@ __device__ __forceinline__ felt add(felt a, felt b) {
   uint32_t s1 = addc_co(x.w1, y.w1, c, c);
   uint32_t s2 = addc_co(x.w2, y.w2, c, c);
   uint32_t s3 = addc_co(x.w3, y.w3, c, c);
-  return canon_from(s0, s1, s2, s3, c);
+  return add_sum(s0, s1, s2, s3, c);
 }
 
 __device__ __forceinline__ felt sub(felt a, felt b) {
@@ -167,7 +187,7 @@ __device__ __forceinline__ felt sub(felt a, felt b) {
   uint32_t d2 = subb_co(x.w2, y.w2, bw, bw);
   uint32_t d3 = subb_co(x.w3, y.w3, bw, bw);
   // on borrow: d - C (mod 2^128) == d + p
-  uint32_t m0 = sel_0_m1(bw), m1 = sel(0u, C1, bw);
+  uint32_t m0 = sel_0_m1(bw), m1 = m0 & C1;
   uint64_t b2;
   uint32_t e0 = sub_co(d0, m0, b2);
   uint32_t e1 = subb_co(d1, m1, b2, b2);
@@ -260,7 +280,7 @@ __device__ __forceinline__ felt reduce(const uint32_t r[8]) {
   // net bit 128 = top - borrow (>= 0 overall); set when top & !borrow
   uint64_t k;
   ZKP_ASM("s_andn2_b64 %0, %1, %2" : "=s"(k) : "s"(top), "s"(b) : "scc");
-  return canon_from(z0, z1, z2, z3, k);
+  return canon_rare(z0, z1, z2, z3, k);
 }
 
 __device__ __forceinline__ felt mul(felt a, felt b) {
@@ -294,7 +314,7 @@ __device__ __forceinline__ felt mul_u32(felt a, uint32_t k) {
   // net bit 128 = c - borrow (the value is >= 0): set when c & !borrow
   uint64_t kk;
   ZKP_ASM("s_andn2_b64 %0, %1, %2" : "=s"(kk) : "s"(c), "s"(b) : "scc");
-  return canon_from(z0, z1, z2, z3, kk);
+  return canon_rare(z0, z1, z2, z3, kk);
 }
 
 
@@ -392,19 +412,15 @@ __device__ __forceinline__ void reduce_x2(const uint32_t r[8], const uint32_t s[
   uint64_t k1, k2;
   ZKP_ASM("s_andn2_b64 %0, %1, %2" : "=s"(k1) : "s"(c), "s"(b) : "scc");
   ZKP_ASM("s_andn2_b64 %0, %1, %2" : "=s"(k2) : "s"(e), "s"(f) : "scc");
-  // canonicalize both (interleaved)
-  uint64_t g1, g2;
-  uint32_t t0 = add_co_m1(z0, g1);
-  uint32_t T0 = add_co_m1(Z0, g2);
-  uint32_t t1 = addc_co(z1, C1, g1, g1);
-  uint32_t T1 = addc_co(Z1, C1, g2, g2);
-  uint32_t t2 = addc_co_0(z2, g1, g1);
-  uint32_t T2 = addc_co_0(Z2, g2, g2);
-  uint32_t t3 = addc_co_0(z3, g1, g1);
-  uint32_t T3 = addc_co_0(Z3, g2, g2);
-  uint64_t m1 = or_mask(k1, g1), m2 = or_mask(k2, g2);
-  out_r = join(sel(z0, t0, m1), sel(z1, t1, m1), sel(z2, t2, m1), sel(z3, t3, m1));
-  out_s = join(sel(Z0, T0, m2), sel(Z1, T1, m2), sel(Z2, T2, m2), sel(Z3, T3, m2));
+  // canonical forms (canon_rare): one scalar branch for both products
+  const uint64_t rare = k1 | k2 | __builtin_amdgcn_ballot_w64(max(z3, Z3) == 0xffffffffu);
+  if (rare) {
+    out_r = canon_from(z0, z1, z2, z3, k1);
+    out_s = canon_from(Z0, Z1, Z2, Z3, k2);
+  } else {
+    out_r = join(z0, z1, z2, z3);
+    out_s = join(Z0, Z1, Z2, Z3);
+  }
 }
 
 __device__ __forceinline__ void mul_x2(felt a, felt b, felt c, felt d, felt& ab, felt& cd) {
@@ -413,190 +429,4 @@ __device__ __forceinline__ void mul_x2(felt a, felt b, felt c, felt d, felt& ab,
   reduce_x2(r, s, ab, cd);
 }
 
-// x + y and x - y with the two carry chains interleaved (the butterfly's add/sub pair)
-__device__ __forceinline__ void addsub(felt a, felt b, felt& sum, felt& diff) {
-  L4 x = split(a), y = split(b);
-  uint64_t c, bw;
-  uint32_t s0 = add_co(x.w0, y.w0, c);
-  uint32_t d0 = sub_co(x.w0, y.w0, bw);
-  uint32_t s1 = addc_co(x.w1, y.w1, c, c);
-  uint32_t d1 = subb_co(x.w1, y.w1, bw, bw);
-  uint32_t s2 = addc_co(x.w2, y.w2, c, c);
-  uint32_t d2 = subb_co(x.w2, y.w2, bw, bw);
-  uint32_t s3 = addc_co(x.w3, y.w3, c, c);
-  uint32_t d3 = subb_co(x.w3, y.w3, bw, bw);
-  uint64_t g, b2;
-  uint32_t m0 = sel_0_m1(bw), m1 = sel(0u, C1, bw);
-  uint32_t t0 = add_co_m1(s0, g);
-  uint32_t e0 = sub_co(d0, m0, b2);
-  uint32_t t1 = addc_co(s1, C1, g, g);
-  uint32_t e1 = subb_co(d1, m1, b2, b2);
-  uint32_t t2 = addc_co_0(s2, g, g);
-  uint32_t e2 = subb_co_0(d2, b2, b2);
-  uint32_t t3 = addc_co_0(s3, g, g);
-  uint32_t e3 = subb_0(d3, b2);
-  uint64_t m = or_mask(c, g);
-  sum = join(sel(s0, t0, m), sel(s1, t1, m), sel(s2, t2, m), sel(s3, t3, m));
-  diff = join(e0, e1, e2, e3);
-}
-
-
-// N independent products with every step issued for all N chains before the
-// next step: each SGPR carry is consumed N instructions after it is produced,
-// so with N >= 3 no s_nop is needed for the carry hazard (N = 2 leaves one
-// wait state per step, which the compiler fills with s_nop 0: ~25% of the
-// NTT's instructions were such nops). Loops have constant trip counts and are
-// fully unrolled, so every array below lives in registers.
-template <int N>
-__device__ __forceinline__ void mul_xn(const felt* a, const felt* b, felt* out) {
-  L4 x[N], y[N];
-  uint32_t r[N][8];
-  uint64_t acc[N], c[N];
-  uint32_t ov[N];
-#pragma unroll
-  for (int k = 0; k < N; k++) { x[k] = split(a[k]); y[k] = split(b[k]); }
-#pragma unroll
-  for (int k = 0; k < N; k++) acc[k] = mul_wide(x[k].w0, y[k].w0);
-#pragma unroll
-  for (int k = 0; k < N; k++) { r[k][0] = (uint32_t)acc[k]; acc[k] >>= 32; }
-  auto wi = [](const L4& v, int i) { return i == 0 ? v.w0 : i == 1 ? v.w1 : i == 2 ? v.w2 : v.w3; };
-  // column col = i + j over the pairs (i, j); first pair starts the overflow word
-#define ZKP_XN_COL(col, ...)                                                            \
-  {                                                                                     \
-    constexpr int pairs[][2] = {__VA_ARGS__};                                           \
-    constexpr int np = sizeof(pairs) / sizeof(pairs[0]);                                \
-    _Pragma("unroll") for (int q = 0; q < np; q++) {                                    \
-      _Pragma("unroll") for (int k = 0; k < N; k++)                                     \
-        acc[k] = mad_co(wi(x[k], pairs[q][0]), wi(y[k], pairs[q][1]), acc[k], c[k]);    \
-      _Pragma("unroll") for (int k = 0; k < N; k++)                                     \
-        ov[k] = q == 0 ? carry_0(c[k]) : addc_0(ov[k], c[k]);                           \
-    }                                                                                   \
-    _Pragma("unroll") for (int k = 0; k < N; k++) {                                     \
-      r[k][col] = (uint32_t)acc[k];                                                     \
-      acc[k] = (acc[k] >> 32) | ((uint64_t)ov[k] << 32);                                \
-    }                                                                                   \
-  }
-  ZKP_XN_COL(1, {0, 1}, {1, 0})
-  ZKP_XN_COL(2, {0, 2}, {1, 1}, {2, 0})
-  ZKP_XN_COL(3, {0, 3}, {1, 2}, {2, 1}, {3, 0})
-  ZKP_XN_COL(4, {1, 3}, {2, 2}, {3, 1})
-  ZKP_XN_COL(5, {2, 3}, {3, 2})
-#undef ZKP_XN_COL
-#pragma unroll
-  for (int k = 0; k < N; k++) acc[k] = mad(x[k].w3, y[k].w3, acc[k]);  // column 6 cannot overflow
-#pragma unroll
-  for (int k = 0; k < N; k++) { r[k][6] = (uint32_t)acc[k]; r[k][7] = (uint32_t)(acc[k] >> 32); }
-  // reduction (as reduce(), N chains interleaved step by step)
-  const uint32_t K = 0x2d00u;
-  uint32_t q0[N], q1[N], q2[N], q3[N], q4[N];
-#pragma unroll
-  for (int k = 0; k < N; k++) {
-    uint64_t t = mul_wide(r[k][4], K);
-    q0[k] = (uint32_t)t;
-    t = mad(r[k][5], K, t >> 32);
-    q1[k] = (uint32_t)t;
-    t = mad(r[k][6], K, t >> 32);
-    q2[k] = (uint32_t)t;
-    t = mad(r[k][7], K, t >> 32);
-    q3[k] = (uint32_t)t;
-    q4[k] = (uint32_t)(t >> 32);
-  }
-  uint64_t cc[N], bb[N];
-  uint32_t s1[N], s2[N], s3[N], s4[N], s5[N], x0[N], x1[N], x2[N], x3[N], x4[N], x5[N];
-#pragma unroll
-  for (int k = 0; k < N; k++) s1[k] = add_co(r[k][1], q0[k], cc[k]);
-#pragma unroll
-  for (int k = 0; k < N; k++) x0[k] = sub_co(r[k][0], r[k][4], bb[k]);
-#pragma unroll
-  for (int k = 0; k < N; k++) s2[k] = addc_co(r[k][2], q1[k], cc[k], cc[k]);
-#pragma unroll
-  for (int k = 0; k < N; k++) x1[k] = subb_co(s1[k], r[k][5], bb[k], bb[k]);
-#pragma unroll
-  for (int k = 0; k < N; k++) s3[k] = addc_co(r[k][3], q2[k], cc[k], cc[k]);
-#pragma unroll
-  for (int k = 0; k < N; k++) x2[k] = subb_co(s2[k], r[k][6], bb[k], bb[k]);
-#pragma unroll
-  for (int k = 0; k < N; k++) s4[k] = addc_co_0(q3[k], cc[k], cc[k]);
-#pragma unroll
-  for (int k = 0; k < N; k++) x3[k] = subb_co(s3[k], r[k][7], bb[k], bb[k]);
-#pragma unroll
-  for (int k = 0; k < N; k++) s5[k] = addc_0(q4[k], cc[k]);
-#pragma unroll
-  for (int k = 0; k < N; k++) x4[k] = subb_co_0(s4[k], bb[k], bb[k]);
-#pragma unroll
-  for (int k = 0; k < N; k++) x5[k] = subb_0(s5[k], bb[k]);
-  uint32_t u0[N], u1[N], y1[N], y2[N], y3[N], z0[N], z1[N], z2[N], z3[N];
-#pragma unroll
-  for (int k = 0; k < N; k++) {
-    uint64_t u = mul_wide(x4[k], K);
-    u0[k] = (uint32_t)u;
-    u1[k] = (uint32_t)(u >> 32) + x5[k] * K;
-  }
-#pragma unroll
-  for (int k = 0; k < N; k++) y1[k] = add_co(x1[k], u0[k], cc[k]);
-#pragma unroll
-  for (int k = 0; k < N; k++) z0[k] = sub_co(x0[k], x4[k], bb[k]);
-#pragma unroll
-  for (int k = 0; k < N; k++) y2[k] = addc_co(x2[k], u1[k], cc[k], cc[k]);
-#pragma unroll
-  for (int k = 0; k < N; k++) z1[k] = subb_co(y1[k], x5[k], bb[k], bb[k]);
-#pragma unroll
-  for (int k = 0; k < N; k++) y3[k] = addc_co_0(x3[k], cc[k], cc[k]);
-#pragma unroll
-  for (int k = 0; k < N; k++) z2[k] = subb_co_0(y2[k], bb[k], bb[k]);
-#pragma unroll
-  for (int k = 0; k < N; k++) z3[k] = subb_co_0(y3[k], bb[k], bb[k]);
-  uint64_t kk[N], g[N];
-#pragma unroll
-  for (int k = 0; k < N; k++) asm("s_andn2_b64 %0, %1, %2" : "=s"(kk[k]) : "s"(cc[k]), "s"(bb[k]) : "scc");
-  uint32_t t0[N], t1[N], t2[N], t3[N];
-#pragma unroll
-  for (int k = 0; k < N; k++) t0[k] = add_co_m1(z0[k], g[k]);
-#pragma unroll
-  for (int k = 0; k < N; k++) t1[k] = addc_co(z1[k], C1, g[k], g[k]);
-#pragma unroll
-  for (int k = 0; k < N; k++) t2[k] = addc_co_0(z2[k], g[k], g[k]);
-#pragma unroll
-  for (int k = 0; k < N; k++) t3[k] = addc_co_0(z3[k], g[k], g[k]);
-#pragma unroll
-  for (int k = 0; k < N; k++) {
-    const uint64_t m = or_mask(kk[k], g[k]);
-    out[k] = join(sel(z0[k], t0[k], m), sel(z1[k], t1[k], m), sel(z2[k], t2[k], m), sel(z3[k], t3[k], m));
-  }
-}
-
-// N independent (x + y, x - y) pairs, step-interleaved like mul_xn
-template <int N>
-__device__ __forceinline__ void addsub_xn(const felt* a, const felt* b, felt* sum, felt* diff) {
-  L4 x[N], y[N];
-  uint64_t c[N], bw[N], g[N], b2[N];
-  uint32_t s0[N], s1[N], s2[N], s3[N], d0[N], d1[N], d2[N], d3[N];
-#pragma unroll
-  for (int k = 0; k < N; k++) { x[k] = split(a[k]); y[k] = split(b[k]); }
-#pragma unroll
-  for (int k = 0; k < N; k++) { s0[k] = add_co(x[k].w0, y[k].w0, c[k]); d0[k] = sub_co(x[k].w0, y[k].w0, bw[k]); }
-#pragma unroll
-  for (int k = 0; k < N; k++) { s1[k] = addc_co(x[k].w1, y[k].w1, c[k], c[k]); d1[k] = subb_co(x[k].w1, y[k].w1, bw[k], bw[k]); }
-#pragma unroll
-  for (int k = 0; k < N; k++) { s2[k] = addc_co(x[k].w2, y[k].w2, c[k], c[k]); d2[k] = subb_co(x[k].w2, y[k].w2, bw[k], bw[k]); }
-#pragma unroll
-  for (int k = 0; k < N; k++) { s3[k] = addc_co(x[k].w3, y[k].w3, c[k], c[k]); d3[k] = subb_co(x[k].w3, y[k].w3, bw[k], bw[k]); }
-  uint32_t m0[N], m1[N], t0[N], t1[N], t2[N], t3[N], e0[N], e1[N], e2[N], e3[N];
-#pragma unroll
-  for (int k = 0; k < N; k++) { m0[k] = sel_0_m1(bw[k]); m1[k] = sel(0u, C1, bw[k]); }
-#pragma unroll
-  for (int k = 0; k < N; k++) { t0[k] = add_co_m1(s0[k], g[k]); e0[k] = sub_co(d0[k], m0[k], b2[k]); }
-#pragma unroll
-  for (int k = 0; k < N; k++) { t1[k] = addc_co(s1[k], C1, g[k], g[k]); e1[k] = subb_co(d1[k], m1[k], b2[k], b2[k]); }
-#pragma unroll
-  for (int k = 0; k < N; k++) { t2[k] = addc_co_0(s2[k], g[k], g[k]); e2[k] = subb_co_0(d2[k], b2[k], b2[k]); }
-#pragma unroll
-  for (int k = 0; k < N; k++) { t3[k] = addc_co_0(s3[k], g[k], g[k]); e3[k] = subb_0(d3[k], b2[k]); }
-#pragma unroll
-  for (int k = 0; k < N; k++) {
-    const uint64_t m = or_mask(c[k], g[k]);
-    sum[k] = join(sel(s0[k], t0[k], m), sel(s1[k], t1[k], m), sel(s2[k], t2[k], m), sel(s3[k], t3[k], m));
-    diff[k] = join(e0[k], e1[k], e2[k], e3[k]);
-  }
-}
 }  // namespace fpd

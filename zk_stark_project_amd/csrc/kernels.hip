@@ -62,7 +62,7 @@ template <int CE>
 __global__ __launch_bounds__(TPB) void k_comp_dft(const felt* __restrict__ recv, const uint32_t* __restrict__ blk,
                                                   const felt* __restrict__ Si, const felt* __restrict__ consts,
                                                   uint32_t C, uint32_t logn, uint64_t p0, uint64_t nR,
-                                                  felt* __restrict__ out) {
+                                                  felt* __restrict__ out, uint32_t* __restrict__ hi_flag) {
   const uint64_t pl = blockIdx.x * (uint64_t)TPB + threadIdx.x;
   if (pl >= nR) return;
   felt x[CE];
@@ -88,6 +88,19 @@ __global__ __launch_bounds__(TPB) void k_comp_dft(const felt* __restrict__ recv,
     constexpr int m = decltype(mm)::value;
     if ((uint32_t)m < C) out[m * nR + pl] = mul(x[kc::rev_const(m, kc::ilog2_const(CE))], consts[m]);
   });
+  // segments C..CE-1 of the interpolated polynomial, which CompositionPoly::new's
+  // segment() drops (`.take(num_cols)`): zero for a trace that satisfies its
+  // constraints. A derived last column (LastCol) equals winterfell's only then, so
+  // any nonzero one raises the flag and the proof is made again without it.
+  if (hi_flag) {
+    uint32_t nz = 0;
+    static_for<0, CE>([&](auto mm) {
+      constexpr int m = decltype(mm)::value;
+      const felt v = x[kc::rev_const(m, kc::ilog2_const(CE))];
+      if ((uint32_t)m >= C) nz |= (uint32_t)((v.lo | v.hi) != 0);
+    });
+    if (__builtin_amdgcn_ballot_w64(nz != 0) && (threadIdx.x & 63) == 0) hi_flag[0] = 1u;
+  }
 }
 
 // coefficient-dependent constants of the constraint evaluation kernels, from cc:
@@ -1112,7 +1125,8 @@ void launch_eval_bitrev(Prof& prof, hipStream_t s, const felt* arrays, uint32_t 
 
 void launch_deep_denominators(Prof& prof, hipStream_t s, const PointMap& m, uint64_t count, const felt* zz,
                               const felt* pw, felt* binv) {
-  if (count & ((1ull << m.logn) - 1)) abort();  // whole cosets only (closed-form total)
+  if (count & ((1ull << m.logn) - 1))  // whole cosets only (closed-form total)
+    launch_fail(ZKP_ERR_DEVICE, "internal: DEEP denominators over a partial coset");
   launch_den_inverse(prof, s, m, count, zero(), zero(), 1, binv, zz, pw);
 }
 
@@ -1138,19 +1152,20 @@ void launch_deep(Prof& prof, hipStream_t s, const DeepArgs& a, felt* out) {
 }
 
 void launch_comp_dft(Prof& prof, hipStream_t s, const felt* recv, const uint32_t* blk, const felt* Si,
-                     const felt* consts, uint32_t ce, uint32_t C, uint32_t logn, uint64_t p0, uint64_t nR, felt* out) {
+                     const felt* consts, uint32_t ce, uint32_t C, uint32_t logn, uint64_t p0, uint64_t nR, felt* out,
+                     uint32_t* hi_flag) {
   const double bytes = (double)nR * (2 * ce + C) * 16.0;
   const dim3 g(blocks_for(nR));
   switch (ce) {
     case 2: LAUNCH(prof, "comp_dft", s, bytes, hipLaunchKernelGGL(k_comp_dft<2>, g, dim3(TPB), 0, s, recv, blk, Si,
-                                                                   consts, C, logn, p0, nR, out)); break;
+                                                                   consts, C, logn, p0, nR, out, hi_flag)); break;
     case 4: LAUNCH(prof, "comp_dft", s, bytes, hipLaunchKernelGGL(k_comp_dft<4>, g, dim3(TPB), 0, s, recv, blk, Si,
-                                                                   consts, C, logn, p0, nR, out)); break;
+                                                                   consts, C, logn, p0, nR, out, hi_flag)); break;
     case 8: LAUNCH(prof, "comp_dft", s, bytes, hipLaunchKernelGGL(k_comp_dft<8>, g, dim3(TPB), 0, s, recv, blk, Si,
-                                                                   consts, C, logn, p0, nR, out)); break;
+                                                                   consts, C, logn, p0, nR, out, hi_flag)); break;
     case 16: LAUNCH(prof, "comp_dft", s, bytes, hipLaunchKernelGGL(k_comp_dft<16>, g, dim3(TPB), 0, s, recv, blk,
-                                                                    Si, consts, C, logn, p0, nR, out)); break;
-    default: abort();  // the prover admits ce <= 16 (ZKP_ERR_UNSUPPORTED_AIR otherwise)
+                                                                    Si, consts, C, logn, p0, nR, out, hi_flag)); break;
+    default: launch_fail(ZKP_ERR_UNSUPPORTED_AIR, "composition DFT supports ce in {2, 4, 8, 16}");
   }
 }
 

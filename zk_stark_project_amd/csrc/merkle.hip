@@ -1174,7 +1174,7 @@ bool launch_merkle_lde(Prof& prof, hipStream_t s, const felt* lde, uint32_t cols
     a.gl = *gl;
     merkle_pass<4>(prof, s, a, H, "merkle_lde", (double)L * (gl->wi * 16.0 + 64.0));
   } else if (lc) {  // the caller checked merkle_can_derive(cols, L)
-    if (H != 1 || cols < 2 || cols > 8) abort();
+    if (H != 1 || cols < 2 || cols > 8) launch_fail(ZKP_ERR_DEVICE, "internal: derived-column leaf shape");
     a.lc = *lc;
     const double bytes = (double)L * (cols * 16.0 + 48.0);
     const dim3 g(blocks_for(L >> 1));
@@ -1298,7 +1298,7 @@ void launch_pack(Prof& prof, hipStream_t s, const PackArgs& a, void* dst) {
 void launch_fri_remainder(Prof& prof, hipStream_t s, const felt* E, uint32_t logB, uint32_t m, felt off_inv,
                           felt wd_inv, felt d_inv, uint32_t* seed, felt* rem_out, uint32_t* commit_out) {
   const uint32_t D = m << logB, ncoef = m;
-  if (D > 256) abort();  // the caller keeps larger remainders on the host
+  if (D > 256) launch_fail(ZKP_ERR_DEVICE, "internal: device remainder over 256 values");  // larger ones stay on the host
   LAUNCH(prof, "coin", s, 0.0,
          hipLaunchKernelGGL(k_fri_remainder, dim3(1), dim3(TPB), 0, s, E, logB, m, off_inv, wd_inv, d_inv, ncoef,
                             seed, rem_out, commit_out));
@@ -1323,9 +1323,10 @@ void launch_fri_fold(Prof& prof, hipStream_t s, const felt* E, uint64_t m16, uin
 }
 
 void launch_fri_tail(Prof& prof, hipStream_t s, const FriTailArgs& a) {
-  if (a.nl > FRI_TAIL_MAX || (a.rem_m << a.logB) > 256) abort();
+  if (a.nl > FRI_TAIL_MAX || (a.rem_m << a.logB) > 256) launch_fail(ZKP_ERR_DEVICE, "internal: FRI tail shape");
   for (uint32_t l = 0; l < a.nl; l++)
-    if (a.ly[l].logm16 + a.logB > 7) abort();  // <= 128 rows: one quad per row in 512 threads
+    if (a.ly[l].logm16 + a.logB > 7)  // <= 128 rows: one quad per row in 512 threads
+      launch_fail(ZKP_ERR_DEVICE, "internal: FRI tail layer over 128 rows");
   LAUNCH(prof, "fri_tail", s, 0.0, hipLaunchKernelGGL(k_fri_tail, dim3(1), dim3(512), 0, s, a));
 }
 
@@ -1350,12 +1351,12 @@ void launch_leaf_hash_shard(Prof& prof, hipStream_t s, int mode, const felt* src
                               logrows, logrr, logK, k, send, lcv, glv));                                          \
     break;
   if (gl) {  // lazy GlobalUpdate columns
-    if (mode != 0) abort();
+    if (mode != 0) launch_fail(ZKP_ERR_DEVICE, "internal: lazy columns in a FRI leaf pass");
     LAUNCH(prof, "leaf_hash_shard", s, (double)cnt * (gl->wi * 16.0 + 32.0),
            hipLaunchKernelGGL(k_leaf_hash_shard<4>, g, dim3(TPB), 0, s, src, n, cols, logBl, logrows, logrr, logK, k,
                               send, lcv, glv));
   } else if (lc) {  // the caller checked merkle_can_derive
-    if (mode != 0 || cols < 2 || cols > 8) abort();
+    if (mode != 0 || cols < 2 || cols > 8) launch_fail(ZKP_ERR_DEVICE, "internal: derived-column shard leaf shape");
     switch (cols) { ZKP_SHARD_LEAFD(2) ZKP_SHARD_LEAFD(3) ZKP_SHARD_LEAFD(4) ZKP_SHARD_LEAFD(5)
                     ZKP_SHARD_LEAFD(6) ZKP_SHARD_LEAFD(7) ZKP_SHARD_LEAFD(8) }
   } else if (mode == 0 && cols <= 8) {

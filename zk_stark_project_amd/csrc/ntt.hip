@@ -124,12 +124,6 @@ __device__ __forceinline__ void bfly(felt& x, felt& y, felt w) {
   }
 }
 
-#ifdef ZKP_EXP_NOBFLY
-#define ZKP_EXP_NOBFLY_ON true
-#else
-#define ZKP_EXP_NOBFLY_ON false
-#endif
-
 // butterfly with twiddle 1 (no product)
 template <bool DIT>
 __device__ __forceinline__ void bfly1(felt& x, felt& y) {
@@ -216,23 +210,11 @@ __global__ __launch_bounds__(NT) void k_ntt8(Ntt8Args a) {
   // 8 XCDs: with B = 8 cosets batch b = col*B + j lands on XCD j, so the
   // columns of a coset share its scale rows and every batch shares the pass's
   // twiddles in that XCD's L2 instead of refetching them per array.
-#ifdef ZKP_NTT_POSFAST
-  const uint32_t bidx = blockIdx.y;  // position blocks fastest in dispatch order
-#else
   const uint32_t bidx = blockIdx.x;
-#endif
   const felt* src = a.src + (uint64_t)(bidx / a.src_div) * a.src_stride;
   felt* dst = a.dst + (uint64_t)bidx * a.dst_stride;
-#ifdef ZKP_EXP_NOSCALE  // timing experiment only: no coset-scale reads (wrong values)
-  const felt* scale = nullptr;
-#else
   const felt* scale = a.scale ? a.scale + ((uint64_t)(bidx % a.scale_mod) << a.logn) : nullptr;
-#endif
-#ifdef ZKP_NTT_POSFAST
-  const uint64_t g0 = (uint64_t)blockIdx.x << logT;
-#else
   const uint64_t g0 = (uint64_t)blockIdx.y << logT;
-#endif
   const uint32_t hi0 = (uint32_t)(g0 >> lo);
   const uint32_t l0 = (Tl == T) ? (uint32_t)(g0 & ((1ull << lo) - 1)) : 0;
   const uint32_t qmask = (1u << K) - 1;
@@ -261,13 +243,8 @@ __global__ __launch_bounds__(NT) void k_ntt8(Ntt8Args a) {
     for (int i = 0; i < 8; i++) {
       uint32_t slot;
       uint32_t ad = staged_elem(tid + i * NT, slot);
-#ifdef ZKP_EXP_NOGMEM
-      felt v = fp::make(ad, (uint64_t)i);
-      if (scale) v = mul(v, v);
-#else
       felt v = src[ad];
       if (scale) v = mul(v, scale[ad]);
-#endif
       lds[slot] = v;
     }
     __syncthreads();
@@ -295,24 +272,15 @@ __global__ __launch_bounds__(NT) void k_ntt8(Ntt8Args a) {
       uint32_t c = (extra << LOGNT) | tid;
       if (first && !staged) {  // straight from HBM (coalesced along gg), coset scale fused
         uint32_t ad = gaddr(coord_gg(m), coord_q(m));
-#ifdef ZKP_EXP_NOGMEM  // timing experiment only (scripts/ntt_experiments.sh): no HBM reads
-        felt v = fp::make(ad, (uint64_t)m);
-        if (scale) v = mul(v, v);
-#else
         felt v = src[ad];
         if (scale) v = mul(v, scale[ad]);
-#endif
         x[m] = v;
       } else {
         x[m] = lds[lidx(coord_q(m), coord_gg(m))];
       }
       if (bf == 0 && extra < 2) { ggs[extra] = c & (T - 1); qlow[extra] = (c >> logT) & ((1u << b0) - 1); }
     }
-#ifdef ZKP_EXP_NOBFLY  // timing experiment only: data movement without butterflies
-    if constexpr (false) {
-#else
     if constexpr (rb == 3) {
-#endif
       const uint32_t l = l0 + (ggs[0] & (Tl - 1));
       const uint32_t jb = (qlow[0] << lo) | l;
       const uint32_t jstep = 1u << (b0 + lo);
@@ -367,7 +335,7 @@ __global__ __launch_bounds__(NT) void k_ntt8(Ntt8Args a) {
           bfly2<false>(x[0], x[1], w0, x[2], x[3], w0); bfly2<false>(x[4], x[5], w0, x[6], x[7], w0);
         }
       }
-    } else if constexpr (rb == 2 && !ZKP_EXP_NOBFLY_ON) {
+    } else if constexpr (rb == 2) {
       if constexpr (!DIT && SMALL && last) {  // DIF stages 1, 0: one product of four is not by 1
         const felt w1 = ntt_tw<false>(a, 1, 1);
 #pragma unroll
@@ -394,7 +362,7 @@ __global__ __launch_bounds__(NT) void k_ntt8(Ntt8Args a) {
         }
       }
       }
-    } else if constexpr (!ZKP_EXP_NOBFLY_ON) {
+    } else {
 #pragma unroll
       for (int u = 0; u < 4; u++) {
         uint32_t c = ((uint32_t)u << LOGNT) | tid;
@@ -407,11 +375,7 @@ __global__ __launch_bounds__(NT) void k_ntt8(Ntt8Args a) {
     if (!last || staged) __syncthreads();  // everyone has read this round's slots
 #pragma unroll
     for (int m = 0; m < 8; m++) {
-#ifdef ZKP_EXP_NOGMEM
-      if (last && !staged && x[m].lo == 0x0123456789abcdefull) dst[gaddr(coord_gg(m), coord_q(m))] = x[m];
-#else
       if (last && !staged) dst[gaddr(coord_gg(m), coord_q(m))] = x[m];  // straight to HBM
-#endif
       else lds[lidx(coord_q(m), coord_gg(m))] = x[m];
     }
     if (DIT) b0 += rb;
@@ -422,11 +386,7 @@ __global__ __launch_bounds__(NT) void k_ntt8(Ntt8Args a) {
     for (int i = 0; i < 8; i++) {
       uint32_t slot;
       uint32_t ad = staged_elem(tid + i * NT, slot);
-#ifdef ZKP_EXP_NOGMEM
-      if (lds[slot].lo == 0x0123456789abcdefull) dst[ad] = lds[slot];
-#else
       dst[ad] = lds[slot];
-#endif
     }
   }
   (void)E;
@@ -512,17 +472,15 @@ static void launch_ntt_radix2(Prof& prof, hipStream_t s, const NttBatch& b, uint
 void launch_ntt(Prof& prof, hipStream_t s, const NttBatch& b, uint32_t logn, bool dit, const felt* tw,
                 uint32_t logN) {
   const uint32_t LOGE = 11;
-#ifndef ZKP_NTT_KMAX
-#define ZKP_NTT_KMAX 8
-#endif
   // passes of up to KMAX stages. 2^17-2^18 run two passes of <= 9 stages instead
   // of three: 9-stage passes use 512-thread blocks of 4096 elements (64 KB LDS,
   // 2 blocks per CU = the same 4 waves/SIMD as 256-thread blocks; strided groups
   // still load 8-felt runs), a third less HBM traffic for the same rounds.
-  // 10-stage passes (2^19-2^20 in two passes, ZKP_NTT_KMAX=10) use the same
-  // 512-thread blocks with rows of 4 felts (see k_ntt8's lidx).
-  const uint32_t KMAX = (logn == 17 || logn == 18) ? 9 : (logn == 19 || logn == 20) ? ZKP_NTT_KMAX : 8;
-  if (logN > 28) abort();  // k_ntt8 indexes arrays and twiddles with 32-bit element offsets
+  // (10-stage passes for 2^19-2^20 — 512-thread blocks with rows of 4 felts, the
+  // T = 4 layout of k_ntt8's lidx — measured slower than 6+6+8: DESIGN.md §4.)
+  const uint32_t KMAX = (logn == 17 || logn == 18) ? 9 : 8;
+  if (logN > 28)  // k_ntt8 indexes arrays and twiddles with 32-bit element offsets
+    launch_fail(ZKP_ERR_TRACE_SHAPE, "NTT domain over 2^28 points (n * blowup)");
   if (logn < LOGE) {
     launch_ntt_radix2(prof, s, b, logn, dit, tw, logN);
     return;
@@ -549,9 +507,7 @@ void launch_ntt(Prof& prof, hipStream_t s, const NttBatch& b, uint32_t logn, boo
         (const void*)k_ntt8<false, 256, 7, true>,  (const void*)k_ntt8<false, 256, 8, true>};
     for (const void* f : fns) (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)maxb);
     const void* k9[] = {(const void*)k_ntt8<true, 512, 9, false>,  (const void*)k_ntt8<false, 512, 9, false>,
-                        (const void*)k_ntt8<true, 512, 9, true>,   (const void*)k_ntt8<false, 512, 9, true>,
-                        (const void*)k_ntt8<true, 512, 10, false>, (const void*)k_ntt8<false, 512, 10, false>,
-                        (const void*)k_ntt8<true, 512, 10, true>,  (const void*)k_ntt8<false, 512, 10, true>};
+                        (const void*)k_ntt8<true, 512, 9, true>,   (const void*)k_ntt8<false, 512, 9, true>};
     for (const void* f : k9) (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 4096 * 16);
     attr_devs |= 1ull << (dev & 63);
   }
@@ -574,8 +530,7 @@ void launch_ntt(Prof& prof, hipStream_t s, const NttBatch& b, uint32_t logn, boo
   uint32_t s0 = 0;
   for (uint32_t p = 0; p < npass; p++) {
     uint32_t K = Ks[p];
-    // 9 stages: 512 threads x 8 = 4096 elements, rows of 8; 10 stages: 512 x 8,
-    // rows of 4 (64 KB either way: 2 blocks per CU)
+    // 9 stages: 512 threads x 8 = 4096 elements, rows of 8 (64 KB: 2 blocks per CU)
     const uint32_t lognt = K >= 9 ? 9 : 8, loge = lognt + 3;
     Ntt8Args a;
     bool first = p == 0;
@@ -605,11 +560,7 @@ void launch_ntt(Prof& prof, hipStream_t s, const NttBatch& b, uint32_t logn, boo
       rem -= rb;
     }
     uint64_t groups = 1ull << (logn - K);
-#ifdef ZKP_NTT_POSFAST
-    dim3 grid((uint32_t)(groups >> a.logT), b.batches);
-#else
     dim3 grid(b.batches, (uint32_t)(groups >> a.logT));  // batch fastest (see k_ntt8)
-#endif
     size_t shmem = (size_t)(1u << K) * (1u << a.logT) * sizeof(felt);
     // compulsory bytes of this launch: every distinct input array once (the
     // coefficient arrays are shared by src_div coset batches, the scale table
@@ -635,9 +586,7 @@ void launch_ntt(Prof& prof, hipStream_t s, const NttBatch& b, uint32_t logn, boo
       case 16: ZKP_NTT8(false, 256, 8); break;
       case 19: ZKP_NTT8(true, 512, 9); break;
       case 18: ZKP_NTT8(false, 512, 9); break;
-      case 21: ZKP_NTT8(true, 512, 10); break;
-      case 20: ZKP_NTT8(false, 512, 10); break;
-      default: abort();  // launch_ntt only plans passes of 5..KMAX stages
+      default: launch_fail(ZKP_ERR_DEVICE, "internal: NTT pass of an unplanned size");
     }
 #undef ZKP_NTT8
     s0 += K;

@@ -1070,8 +1070,12 @@ struct ProofRun {
   unsigned long long dnonce = ~0ull;
   static constexpr uint64_t grind_chunk = 1ull << 22;
   uint64_t nonce = 0;
-  // GlobalUpdate column pairing (trace_stage): world 1 only
-  bool allow_pair = true, paired = false;
+  // exact shortcuts whose result rests on the trace satisfying its constraints
+  // (GlobalUpdate column pairing, the derived last composition column): the first
+  // attempt takes them and checks on the device; a failed check proves again without
+  bool allow_shortcuts = true;
+  // GlobalUpdate column pairing (trace_stage)
+  bool paired = false;
   felt* gu_cval = nullptr;
   uint32_t* gu_bad = nullptr;    // this rank's check flag (4 words)
   uint32_t* gu_flags = nullptr;  // column-sharded: every rank's flags (all-gathered)
@@ -1082,6 +1086,13 @@ struct ProofRun {
   GuLazy gu_lazy{};
   const felt* l0_table();
   bool pair_failed();
+  // derived last composition column (LastCol, constraint_stage): the segments that
+  // CompositionPoly::new drops must be zero (k_comp_dft raises lc_bad otherwise)
+  bool derive_last = false;
+  uint32_t* lc_bad = nullptr;    // this rank's flag (4 words)
+  uint32_t* lc_flags = nullptr;  // sharded: every rank's flags (all-gathered)
+  bool lastcol_failed();
+  bool h_partial = false;  // a host trace of which only this rank's columns were uploaded
 
   ProofRun(zkp_ctx* c, zkp_comm* m, const zkp_proof_options* opts)
       : ctx(c), cm(m), o(opts), st(c->stream), pf(c->prof) {
@@ -1120,7 +1131,7 @@ int ProofRun::init(int air_id, const felt* d_trace_in, uint32_t width, uint64_t 
   B = o->blowup_factor; F = o->fri_folding_factor;
   logn = ilog2(n); logB = ilog2(B); logN = logn + logB;
   N = 1ull << logN;
-  if (logN > 32) return ZKP_ERR_TRACE_SHAPE;
+  if (logN > MAX_LOG_DOMAIN || logn > MAX_LOG_TRACE) return ZKP_ERR_TRACE_SHAPE;
   // coset sharding: rank r owns the LDE cosets [j0, j0 + Bl)
   R = (uint32_t)cm->world; rank = (uint32_t)cm->rank;
   if (R == 0 || (R & (R - 1)) || R > B || rank >= R) return ZKP_ERR_ARGUMENT;
@@ -1198,7 +1209,7 @@ void ProofRun::trace_stage(const zkp_felt* h_trace) {
   // shortcut. Sharded proofs pair device-resident traces (every rank holds the
   // whole trace; a host trace uploads only the rank's share).
   static const bool no_pair = getenv("ZKP_NO_GU_PAIR") != nullptr;  // A/B switch
-  paired = allow_pair && !no_pair && air.id == ZKP_AIR_GLOBAL_UPDATE && w == 2 * GU_D && (R == 1 || !h_trace);
+  paired = allow_shortcuts && !no_pair && air.id == ZKP_AIR_GLOBAL_UPDATE && w == 2 * GU_D && (R == 1 || !h_trace);
   const uint32_t d = w / 2;
   // wide traces shard the interpolation by column (cpt columns per rank) when the
   // width divides over the ranks; narrow ones interpolate on every rank
@@ -1243,8 +1254,10 @@ void ProofRun::trace_stage(const zkp_felt* h_trace) {
     for (uint32_t k = 0; k < K; k++) {
       const uint64_t cown = (uint64_t)k * R * cpr + (uint64_t)rank * cpr, c0 = (uint64_t)k * R * cpr;
       felt* dcol = const_cast<felt*>(d_trace) + cown * n;
-      if (h_trace)
+      if (h_trace) {
         HIP_CHECK(hipMemcpyAsync(dcol, h_trace + cown * n, (size_t)cpr * n * 16, hipMemcpyHostToDevice, ctx->copy));
+        h_partial = true;
+      }
       NttBatch ib{dcol, own + (size_t)k * cpr * n, nullptr, n, n, 1, 1, cpr};
       launch_ntt(pf, ctx->copy, ib, logn, false, ctx->itws(logN), logN);
       HIP_CHECK(hipEventRecord(ctx->up_ev[k], ctx->copy));
@@ -1415,7 +1428,12 @@ void ProofRun::constraint_stage() {
     // the last composition column derived in the leaf pass (LastCol): the rank's
     // LDE cosets are exactly its CE cosets, whose evaluations stay in `comp`
     static const bool no_derive = getenv("ZKP_NO_DERIVE_LAST") != nullptr;  // A/B switch
-    const bool derive = !no_derive && logce == logB && C >= 2 && C <= 8 && cel == Bl && u0 == j0;
+    const bool derive = allow_shortcuts && !no_derive && logce == logB && C >= 2 && C <= 8 && cel == Bl && u0 == j0;
+    derive_last = derive;
+    if (derive) {
+      lc_bad = ctx->buf<uint32_t>("lc_bad", 4);
+      HIP_CHECK(hipMemsetAsync(lc_bad, 0, 16, st));
+    }
     felt* cint = derive ? ctx->buf<felt>("comp_int", (size_t)(cel ? cel : 1) * n) : comp;
     if (cel) {
       NttBatch ib{comp, cint, nullptr, n, n, 1, 1, cel};
@@ -1448,7 +1466,12 @@ void ProofRun::constraint_stage() {
       ctx->upload(dblk, blk.data(), blk.size() * 4);
     }
     felt* slice = R > 1 ? ctx->buf<felt>("comp_ag_send", (size_t)C * nR) : acoef;
-    launch_comp_dft(pf, st, recv, dblk, ctx->Si(logn, logB, logce), dcoefs, ce, C, logn, p0, nR, slice);
+    launch_comp_dft(pf, st, recv, dblk, ctx->Si(logn, logB, logce), dcoefs, ce, C, logn, p0, nR, slice,
+                    derive ? lc_bad : nullptr);
+    if (R > 1 && derive) {  // every rank's check of its position slice
+      lc_flags = ctx->buf<uint32_t>("lc_flags", 4 * (size_t)R);
+      cm->all_gather(st, lc_bad, lc_flags, 16);
+    }
     if (R > 1) {
       // column by column: the all-gather of coefficient column m (rank s's slice of
       // positions [s*nR, (s+1)*nR) lands at acoef + m*n + s*nR, i.e. the column in
@@ -1917,6 +1940,17 @@ bool ProofRun::pair_failed() {
   return false;
 }
 
+// a derived last composition column whose dropped segments were not zero (the trace
+// does not satisfy its constraints): one 16-byte read after the proof's last kernels
+bool ProofRun::lastcol_failed() {
+  if (!derive_last) return false;
+  std::vector<uint32_t> f(lc_flags ? 4 * (size_t)R : 4);
+  ctx->download(f.data(), lc_flags ? lc_flags : lc_bad, f.size() * 4);
+  for (uint32_t v : f)
+    if (v) return true;
+  return false;
+}
+
 // h_trace (nullable): the trace is still in host memory and d_trace is its
 // device buffer; the upload is pipelined with the trace interpolation and LDE
 // by column groups (wide traces), so PCIe overlaps the first stage's kernels.
@@ -1925,7 +1959,7 @@ int prove_impl(zkp_ctx* ctx, zkp_comm* cm, int air_id, const felt* d_trace, uint
                uint64_t* proof_len, zkp_transcript* tr_out, const zkp_felt* h_trace = nullptr) {
   for (int attempt = 0;; attempt++) {
     ProofRun run(ctx, cm, o);
-    run.allow_pair = attempt == 0;
+    run.allow_shortcuts = attempt == 0;
     int rc = run.init(air_id, d_trace, w, n, pub_elems, n_pub, proof, proof_len);
     if (rc) return rc;
     run.setup();
@@ -1935,15 +1969,31 @@ int prove_impl(zkp_ctx* ctx, zkp_comm* cm, int air_id, const felt* d_trace, uint
     run.deep_stage();
     run.fri_stage();
     run.grind_stage();
-    // the paired columns rest on the trace's transitions: if they do not hold, prove
-    // the (now device-resident) trace again without the pairing
-    if (run.pair_failed()) {
-      h_trace = nullptr;
+    // the paired columns and the derived composition column rest on the trace's
+    // constraints: if they do not hold, prove the (now device-resident) trace again
+    // without the shortcuts
+    if (run.pair_failed() || run.lastcol_failed()) {
+      if (!run.h_partial) h_trace = nullptr;  // resident from here
       continue;
     }
     return run.finish(proof, proof_len, tr_out);
   }
 }
+
+// every stream of the context idle: nothing queued by a failed call (a late
+// upload, a check writing its flag, a column round) may run into the next call's
+// buffers or outlive the context
+void drain_streams(zkp_ctx* ctx) {
+  (void)hipStreamSynchronize(ctx->copy);
+  (void)hipStreamSynchronize(ctx->side);
+  (void)hipStreamSynchronize(ctx->stream);
+}
+
+}  // namespace
+
+void launch_fail(int code, const char* what) { throw ZkpFail{code, what}; }
+
+namespace {
 
 template <typename F>
 int guarded(zkp_ctx* ctx, F&& f) {
@@ -1955,16 +2005,20 @@ int guarded(zkp_ctx* ctx, F&& f) {
   } catch (const ZkpFail& e) {
     ctx->err = e.msg;
     ctx->prof.pending.clear();
+    drain_streams(ctx);
     return e.code;
   } catch (const std::bad_alloc&) {
     ctx->err = "host out of memory";
+    drain_streams(ctx);
     return ZKP_ERR_OOM;
   } catch (const CommError& e) {
     ctx->err = std::string("collective failed: ") + e.what();
     ctx->prof.pending.clear();
+    drain_streams(ctx);
     return ZKP_ERR_DEVICE;
   } catch (...) {
     ctx->err = "unknown failure";
+    drain_streams(ctx);
     return ZKP_ERR_DEVICE;
   }
 }
@@ -2001,7 +2055,7 @@ int zkp_ctx_create(int device, zkp_ctx** out) {
 void zkp_ctx_destroy(zkp_ctx* ctx) {
   if (!ctx) return;
   (void)hipSetDevice(ctx->device);
-  (void)hipStreamSynchronize(ctx->stream);
+  drain_streams(ctx);
   delete ctx;
 }
 
@@ -2199,6 +2253,7 @@ int zkp_trace_lde_commit(zkp_ctx* ctx, const zkp_felt* trace, uint32_t w, uint64
     if (n < 8 || (n & (n - 1)) || w == 0 || w > 255) return (int)ZKP_ERR_TRACE_SHAPE;
     if (blowup < 2 || (blowup & (blowup - 1)) || blowup > 128) return (int)ZKP_ERR_INVALID_OPTIONS;
     uint32_t logn = ilog2(n), logB = ilog2(blowup);
+    if (logn + logB > MAX_LOG_DOMAIN) return (int)ZKP_ERR_TRACE_SHAPE;
     uint64_t N = n * blowup;
     felt* d = ctx->buf<felt>("trace_in", (size_t)w * n);
     ctx->upload(d, trace, (size_t)w * n * 16);
@@ -2438,7 +2493,7 @@ int zkp_session_create(zkp_ctx* ctx, zkp_air_id air_id, uint32_t width, uint64_t
     if (s->ce > 16 || s->C > s->ce) return (int)ZKP_ERR_UNSUPPORTED_AIR;
     s->logn = ilog2(n); s->logB = ilog2(s->B); s->logce = ilog2(s->ce); s->logN = s->logn + s->logB;
     s->N = n << s->logB;
-    if (s->logN > 32) return (int)ZKP_ERR_TRACE_SHAPE;
+    if (s->logN > MAX_LOG_DOMAIN || s->logn > MAX_LOG_TRACE) return (int)ZKP_ERR_TRACE_SHAPE;
     uint64_t D = s->N, maxrem = (uint64_t)(o->fri_remainder_max_degree + 1) * s->B;
     while (D > maxrem) { D /= s->F; s->L++; }
     s->pfx = "sess" + std::to_string(ctx->next_session++) + "_";

@@ -27,6 +27,15 @@ struct Prof {
   void end(hipStream_t s);
 };
 
+// A launch the kernels cannot take (a shape past their 32-bit offsets, a broken
+// internal invariant): thrown as the calling entry point's ZKP_ERR_* status
+// (prover.cpp), never an abort() across the C ABI.
+[[noreturn]] void launch_fail(int code, const char* what);
+// largest LDE domain (n * blowup) the NTT passes index with 32-bit element
+// offsets, and the largest trace the OOD evaluation's block tree takes; entry
+// points return ZKP_ERR_TRACE_SHAPE past them
+constexpr uint32_t MAX_LOG_DOMAIN = 28, MAX_LOG_TRACE = 23;
+
 // ---------------------------------------------------------------- NTT
 // One LDS pass of K radix-2 stages (see kernels.hip). `dit` = bit-reversed in
 // -> natural out (Cooley-Tukey); otherwise natural in -> bit-reversed out
@@ -279,7 +288,8 @@ void launch_gu_fill(Prof& prof, hipStream_t s, felt* lde, uint32_t w, uint32_t l
 // bit-reversed positions [p0, p0 + nR), n * c_m = (sum_u Si_u * W_u * w_ce^-um) * g^-mn / ce;
 // consts = [g^-mn / ce for m < C | w_ce^-k for k < ce/2] (ce in {2, 4, 8, 16})
 void launch_comp_dft(Prof& prof, hipStream_t s, const felt* recv, const uint32_t* blk, const felt* Si,
-                     const felt* consts, uint32_t ce, uint32_t C, uint32_t logn, uint64_t p0, uint64_t nR, felt* out);
+                     const felt* consts, uint32_t ce, uint32_t C, uint32_t logn, uint64_t p0, uint64_t nR, felt* out,
+                     uint32_t* hi_flag = nullptr);
 
 // OOD evaluation of bit-reversed arrays (arrays contiguous, stride n) at x0 and x1
 // partial[(a * nblocks + b) * 2 + {0,1}] ; pw0/pw1 = x^(2^l) tables (logn entries, device)
