@@ -379,6 +379,32 @@ def sharded_leg(ctx, rank: int, world: int, dist, local_rank: int, on_timeout=No
             "bytes_per_proof_8d": sum(stage_bytes(1, 1 << 22, 8, 8, 6).values())}
 
 
+NUM_COEFFS = {"mimc": 3, "agg": 180}  # ConstraintCompositionCoefficients: transitions + assertions
+
+
+def session_leg(ctx, wl, pub, tr, steps: int) -> dict:
+    """ms per proof through the stage hooks (zkp_session_* + zkp_channel_*, the route
+    of DESIGN.md §1 that keeps winterfell's Prover::prove), host trace in, openings
+    out; checked against the zkp_prove transcript of the same trace."""
+    from zk_stark_project_amd import _native
+    air = "mimc" if wl["air_id"] == 1 else "agg"
+
+    def once():
+        return _native.prove_by_stages(ctx, wl["air_id"], wl["trace"].data, pub, wl["opts"], NUM_COEFFS[air])
+    got = once()  # warm (the session context's domain tables)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        got = once()
+    ms = (time.perf_counter() - t0) / steps * 1e3
+    want = tr.summary()
+    same = (got["trace_root"].hex() == want["trace_root"] and got["constraint_root"].hex() == want["constraint_root"]
+            and [r.hex() for r in got["fri_roots"]] == want["fri_roots"] and got["z"] == want["z"]
+            and got["pow_nonce"] == want["pow_nonce"] and got["query_positions"] == want["query_positions"])
+    return {"session_ms": round(ms, 3), "steps": steps, "equals_zkp_prove_transcript": same,
+            "route": "zkp_session_trace_lde -> zkp_eval_constraints -> zkp_composition_commit -> zkp_ood_frame -> "
+                     "zkp_deep_fri -> zkp_grind -> zkp_query, coefficients from zkp_channel (host)"}
+
+
 def sharded_self_check(ctx, wl, pub, proof, rank: int, world: int, dist, local_rank: int) -> dict:
     """After the timed sharded proofs (outside the timed region): every rank checks its
     last proof with the product verifier (zkp_verify) and hashes its bytes; rank 0 also
@@ -498,6 +524,9 @@ def main():
         prove_once()
         sus_n += 1
     sus_s = time.perf_counter() - t1
+    # the stage-hook route (a winter-prover fork keeping Prover::prove): the same proof
+    # through zkp_session_* with the host channel drawing every coefficient
+    session = None if sharded else session_leg(ctx, wl, pub, tr, min(args.steps, 10))
     # the oracle's verifier (CPU) runs after every timed region, so the GPU does not
     # sit idle (and clock down) just before the timed steps
     verified = None
@@ -632,6 +661,7 @@ def main():
         "device_resident_ms": round(el_dev / args.steps * 1e3, 3),
         "first_proof_ms": round(first_ms, 3),
         "sustained": {"proofs": sus_n, "seconds": round(sus_s, 3), "proofs_per_s": round(sus_n / sus_s, 3)},
+        "session": session,
         "roofline": roofline,
         # every launch of the two profiled proofs (HIP events per launch, side stream included)
         "launches": {"per_proof": sum(v["launches"] for v in kernels.values()) / 2,

@@ -260,6 +260,28 @@ int zkp_deep_fri(zkp_session* s, const zkp_felt* deep_coeffs, zkp_fri_channel ch
  * paths | u8(L) | per FRI layer: values | batch paths. Free with zkp_free. */
 int zkp_query(zkp_session* s, const uint64_t* positions, uint64_t n_positions, uint8_t** out, uint64_t* out_len);
 
+/* ---- host channel for stage sessions -------------------------------------
+ * ≙ winter-prover 0.12 ProverChannel over DefaultRandomCoin<Blake3_256>, seeded as
+ * generate_proof seeds it (Context::to_elements() || pub_inputs.to_elements(), the
+ * same seed as zkp_prove's transcript). A winter-prover fork keeps its own channel;
+ * a C or Python caller of the session stages draws from this one. Host-only. */
+typedef struct zkp_channel zkp_channel;
+int zkp_channel_create(zkp_air_id air, uint32_t width, uint64_t n, const zkp_felt* pub_elems, uint64_t n_pub,
+                       const zkp_proof_options* opts, zkp_channel** out);
+void zkp_channel_destroy(zkp_channel* ch);
+/* reseed(root): a commitment (trace, constraint, FRI layer, remainder) */
+int zkp_channel_commit(zkp_channel* ch, const uint8_t root[32]);
+/* reseed(hash_elements(els)): the OOD frame, trace part (T(z) || T(z*g)) then composition part */
+int zkp_channel_commit_felts(zkp_channel* ch, const zkp_felt* els, uint64_t n);
+/* count coefficients drawn with `method` (ZKP_BATCHING_*: ConstraintCompositionCoefficients,
+ * DeepCompositionCoefficients), or with count = 0 one element (the OOD point z, a FRI alpha) */
+int zkp_channel_draw(zkp_channel* ch, uint32_t method, uint32_t count, zkp_felt* out);
+/* the coin's seed (the grinding seed for zkp_grind after the remainder commitment) */
+int zkp_channel_seed(const zkp_channel* ch, uint8_t seed[32]);
+/* query positions: draw_integers(num_queries, n*blowup, nonce), sorted and deduplicated;
+ * out holds num_queries values, *n_unique receives the count kept */
+int zkp_channel_query_positions(zkp_channel* ch, uint64_t nonce, uint64_t* out, uint32_t* n_unique);
+
 /* ---- verification (≙ winterfell `verify`) ------------------------------ */
 /* Status codes of zkp_verify; values map onto winter-verifier `VerifierError`. */
 typedef enum zkp_verify_status {

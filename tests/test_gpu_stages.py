@@ -127,3 +127,109 @@ def test_stages_c3_shape(ctx):
     p = gu_prover(64, 1 << 18, opts, seed=3)
     trace = p.build_trace()
     run_stages(ctx, AIR_GLOBAL_UPDATE, trace, p.get_pub_inputs(trace).to_elements(), opts, 2, 1)
+
+
+# ---------------------------------------------------------------- host channel
+NUM_COEFFS = {AIR_MIMC: 3, AIR_GLOBAL_UPDATE: 180, AIR_TRAINING_UPDATE: 480}
+
+
+def check_by_stages(ctx, air_id, data, pub, opts):
+    """zkp_prove vs the same proof made through the stage hooks with the host channel
+    (zkp_channel_*): every commitment, z, the nonce, the positions and the openings."""
+    gpu, tr = ctx.prove(air_id, data, pub, opts)
+    want = tr.summary()
+    got = _native.prove_by_stages(ctx, air_id, data, pub, opts, NUM_COEFFS[air_id])
+    assert got["trace_root"].hex() == want["trace_root"]
+    assert got["constraint_root"].hex() == want["constraint_root"]
+    assert got["z"] == want["z"]
+    assert [r.hex() for r in got["fri_roots"]] == want["fri_roots"]
+    assert got["remainder_commitment"].hex() == want["remainder_commitment"]
+    assert got["pow_nonce"] == want["pow_nonce"]
+    assert got["query_positions"] == want["query_positions"]
+    sec = sections(gpu)
+    assert got["queries"] == sec["queries"] + sec["fri_queries"]
+    return gpu
+
+
+@pytest.mark.parametrize("n,blowup", [(1 << 12, 8), (1 << 13, 16)])
+def test_channel_stages_mimc(ctx, n, blowup):
+    opts = ProofOptions(40, blowup, 10)
+    p, trace = mimc_case(n, opts)
+    check_by_stages(ctx, AIR_MIMC, trace.data, p.get_pub_inputs(trace).to_elements(), opts)
+
+
+@pytest.mark.parametrize("edit", ["transition", "wrong_result"])
+def test_channel_stages_mimc_invalid(ctx, edit):
+    """The session's derived last column: a trace that breaks its constraints is
+    committed again with the column extended (read before the root is returned)."""
+    opts = ProofOptions(40, 8, 8)
+    n = 1 << 11
+    p, trace = mimc_case(n, opts)
+    pub = list(p.get_pub_inputs(trace).to_elements())
+    data = np.array(trace.data, copy=True)
+    if edit == "transition":
+        data[0, 77, 0] ^= np.uint64(0x99)
+    else:
+        pub[1] = (pub[1] + 1) % (2**128 - 45 * 2**40 + 1)
+    gpu = check_by_stages(ctx, AIR_MIMC, data, pub, opts)
+    ref, _ = O.prove(AIR_MIMC, data.tobytes(), 1, n, to_bytes(pub), opts)
+    assert gpu == ref
+
+
+@pytest.mark.parametrize("edit", [None, "transition"])
+def test_channel_stages_global_update(ctx, edit):
+    """GlobalUpdate through the session: paired columns (checked before the trace root
+    is returned) or, for a broken transition, the unpaired trace stage."""
+    opts = ProofOptions(40, 16, 8)
+    n = 1 << 11
+    p = gu_prover(30, n, opts, seed=5)
+    trace = p.build_trace()
+    pub = p.get_pub_inputs(trace).to_elements()
+    data = np.array(trace.data, copy=True)
+    if edit:
+        data[70, 9, 0] ^= np.uint64(0x5A)
+    gpu = check_by_stages(ctx, AIR_GLOBAL_UPDATE, data, pub, opts)
+    ref, _ = O.prove(AIR_GLOBAL_UPDATE, data.tobytes(), 120, n, to_bytes(pub), opts)
+    assert gpu == ref
+
+
+def test_channel_stages_training_update(ctx):
+    from test_training import tu_prover
+    opts = ProofOptions(40, 16, 4)
+    p = tu_prover(2, seed=9, options=opts)
+    tr = p.build_trace()
+    check_by_stages(ctx, AIR_TRAINING_UPDATE, tr.data, p.get_pub_inputs(tr).to_elements(), opts)
+
+
+def test_session_survives_interleaved_prove(ctx):
+    """A session's device state lives on a context of its own: a zkp_prove on the
+    caller's context between two stages does not disturb it."""
+    opts = ProofOptions(40, 8, 4)
+    p, trace = mimc_case(1 << 10, opts)
+    pub = p.get_pub_inputs(trace).to_elements()
+    gpu, tr = ctx.prove(AIR_MIMC, trace.data, pub, opts)
+    ch = _native.Channel(AIR_MIMC, 1, 1 << 10, pub, opts)
+    s = _native.Session(ctx, AIR_MIMC, 1, 1 << 10, pub, opts)
+    try:
+        root = s.trace_lde(trace.data)
+        ctx.prove(AIR_MIMC, mimc_case(1 << 10, opts)[1].data, pub, opts)  # same buffer names on ctx
+        p2, t2 = mimc_case(1 << 11, opts)
+        ctx.prove(AIR_MIMC, t2.data, p2.get_pub_inputs(t2).to_elements(), opts)
+        ch.commit(root)
+        s.eval_constraints(ch.draw_coeffs(opts.batching_constraints, 3), want_evals=False)
+        assert s.composition_commit().hex() == tr.summary()["constraint_root"]
+    finally:
+        s.close()
+        ch.close()
+
+
+@pytest.mark.slow
+def test_channel_stages_c2_c3(ctx):
+    """C2 and C3 shapes through the stage hooks + host channel == zkp_prove."""
+    opts = ProofOptions(40, 8, 21)
+    p, trace = mimc_case(1 << 20, opts)
+    check_by_stages(ctx, AIR_MIMC, trace.data, p.get_pub_inputs(trace).to_elements(), opts)
+    opts = ProofOptions.reference()
+    p = gu_prover(64, 1 << 18, opts, seed=3)
+    trace = p.build_trace()
+    check_by_stages(ctx, AIR_GLOBAL_UPDATE, trace.data, p.get_pub_inputs(trace).to_elements(), opts)

@@ -77,6 +77,8 @@ EXPORTED = [
     "zkp_session_create", "zkp_session_destroy", "zkp_session_trace_lde", "zkp_eval_constraints",
     "zkp_composition_commit", "zkp_ood_frame", "zkp_deep_fri", "zkp_query", "zkp_comm_host_create",
     "zkp_session_shape",
+    "zkp_channel_create", "zkp_channel_destroy", "zkp_channel_commit", "zkp_channel_commit_felts",
+    "zkp_channel_draw", "zkp_channel_seed", "zkp_channel_query_positions",
 ]
 
 # zkp_host_transport callbacks (include/zkp.h)
@@ -179,6 +181,14 @@ def load():
         L.zkp_ood_frame.argtypes = [vp, Felt, vp, vp]
         L.zkp_deep_fri.argtypes = [vp, vp, FRI_CHANNEL, vp, vp, ctypes.POINTER(u64), ctypes.c_char_p]
         L.zkp_query.argtypes = [vp, ctypes.POINTER(u64), u64, ctypes.POINTER(pu8), ctypes.POINTER(u64)]
+        L.zkp_channel_create.argtypes = [i32, u32, u64, vp, u64, popt, ctypes.POINTER(vp)]
+        L.zkp_channel_destroy.argtypes = [vp]
+        L.zkp_channel_destroy.restype = None
+        L.zkp_channel_commit.argtypes = [vp, ctypes.c_char_p]
+        L.zkp_channel_commit_felts.argtypes = [vp, vp, u64]
+        L.zkp_channel_draw.argtypes = [vp, u32, u32, vp]
+        L.zkp_channel_seed.argtypes = [vp, ctypes.c_char_p]
+        L.zkp_channel_query_positions.argtypes = [vp, u64, ctypes.POINTER(u64), ctypes.POINTER(u32)]
         _lib = L
         return L
 
@@ -571,3 +581,100 @@ class Session:
         data = ctypes.string_at(out, olen.value)
         self.lib.zkp_free(out)
         return data
+
+
+class Channel:
+    """`zkp_channel` (include/zkp.h): winter-prover's ProverChannel over
+    DefaultRandomCoin<Blake3_256>, seeded as generate_proof seeds it. Host-only."""
+
+    def __init__(self, air_id: int, width: int, n: int, pub, options: ProofOptions):
+        self.lib = load()
+        self.options = options
+        self.ptr = ctypes.c_void_p()
+        pb = _felts(pub) if len(pub) else None
+        rc = self.lib.zkp_channel_create(air_id, width, n, pb.ctypes.data if pb is not None else None, len(pub),
+                                         ctypes.byref(options.to_c()), ctypes.byref(self.ptr))
+        if rc:
+            raise ZkpError(rc, "zkp_channel_create")
+
+    def close(self):
+        if self.ptr:
+            self.lib.zkp_channel_destroy(self.ptr)
+            self.ptr = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _ok(self, rc, what):
+        if rc:
+            raise ZkpError(rc, what)
+
+    def commit(self, root: bytes):
+        self._ok(self.lib.zkp_channel_commit(self.ptr, bytes(root)), "zkp_channel_commit")
+
+    def commit_felts(self, vals):
+        a = _felts(vals)
+        self._ok(self.lib.zkp_channel_commit_felts(self.ptr, a.ctypes.data, len(vals)), "zkp_channel_commit_felts")
+
+    def draw(self) -> int:
+        out = np.zeros((1, 2), dtype=np.uint64)
+        self._ok(self.lib.zkp_channel_draw(self.ptr, 0, 0, out.ctypes.data), "zkp_channel_draw")
+        return _ints(out)[0]
+
+    def draw_coeffs(self, method: int, count: int) -> list:
+        out = np.zeros((count, 2), dtype=np.uint64)
+        self._ok(self.lib.zkp_channel_draw(self.ptr, method, count, out.ctypes.data), "zkp_channel_draw")
+        return _ints(out)
+
+    def seed(self) -> bytes:
+        b = ctypes.create_string_buffer(32)
+        self._ok(self.lib.zkp_channel_seed(self.ptr, b), "zkp_channel_seed")
+        return b.raw
+
+    def query_positions(self, nonce: int) -> list:
+        out = (ctypes.c_uint64 * 256)()
+        nu = ctypes.c_uint32()
+        self._ok(self.lib.zkp_channel_query_positions(self.ptr, nonce, out, ctypes.byref(nu)),
+                 "zkp_channel_query_positions")
+        return [int(out[i]) for i in range(nu.value)]
+
+
+def prove_by_stages(ctx: "Context", air_id: int, trace: np.ndarray, pub, options: ProofOptions,
+                    num_coeffs: int) -> dict:
+    """One proof through the stage hooks, in generate_proof's order, with the host
+    channel drawing every coefficient (what a winter-prover fork's `Prover::prove`
+    does with its own channel). Returns the commitments, z, nonce, positions and the
+    query section; they equal zkp_prove's for the same trace."""
+    w, n = int(trace.shape[0]), int(trace.shape[1])
+    ch = Channel(air_id, w, n, pub, options)
+    s = Session(ctx, air_id, w, n, pub, options)
+    try:
+        troot = s.trace_lde(trace)
+        ch.commit(troot)
+        s.eval_constraints(ch.draw_coeffs(options.batching_constraints, num_coeffs), want_evals=False)
+        croot = s.composition_commit()
+        ch.commit(croot)
+        z = ch.draw()
+        tood, cood = s.ood_frame(z)
+        ch.commit_felts(tood)
+        ch.commit_felts(cood)
+        gam = ch.draw_coeffs(options.batching_deep, w + s.num_columns)
+        roots = []
+
+        def fri_channel(layer, root):
+            roots.append(root)
+            ch.commit(root)
+            return ch.draw()
+        rem, rcommit = s.deep_fri(gam, fri_channel)
+        ch.commit(rcommit)
+        nonce = ctx.grind(ch.seed(), options.grinding_factor) if options.grinding_factor else 1
+        pos = ch.query_positions(nonce)
+        queries = s.query(pos)
+    finally:
+        s.close()
+        ch.close()
+    return {"trace_root": troot, "constraint_root": croot, "z": z, "fri_roots": roots, "remainder": rem,
+            "remainder_commitment": rcommit, "pow_nonce": nonce, "query_positions": pos, "queries": queries}

@@ -273,7 +273,10 @@ struct zkp_ctx {
     for (auto it = cached.begin(); it != cached.end();)
       it = it->first.compare(0, prefix.size(), prefix) == 0 ? cached.erase(it) : std::next(it);
   }
-  uint64_t next_session = 0;
+  // stage sessions run on contexts of their own (own streams and buffers, so a
+  // session's state survives zkp_prove calls on this context between its stages);
+  // idle ones are kept here with their domain tables for the next session
+  std::vector<zkp_ctx*> session_pool;
   std::vector<hipEvent_t> up_ev;  // pipeline events (column-group uploads, per-column all-gathers)
   void events(size_t k) {  // grows only: events already recorded may still be waited on
     while (up_ev.size() < k) {
@@ -1093,6 +1096,9 @@ struct ProofRun {
   uint32_t* lc_flags = nullptr;  // sharded: every rank's flags (all-gathered)
   bool lastcol_failed();
   bool h_partial = false;  // a host trace of which only this rank's columns were uploaded
+  // stage sessions (zkp_session_*): the caller's channel draws every coefficient, so
+  // commitments return their roots to the host and no device transcript runs
+  bool host_channel = false;
 
   ProofRun(zkp_ctx* c, zkp_comm* m, const zkp_proof_options* opts)
       : ctx(c), cm(m), o(opts), st(c->stream), pf(c->prof) {
@@ -1109,6 +1115,9 @@ struct ProofRun {
   void setup();
   void trace_stage(const zkp_felt* h_trace);
   void constraint_stage();
+  void eval_stage();
+  void composition_stage();
+  void ood_values();
   void ood_stage();
   void deep_stage();
   void fri_stage();
@@ -1400,24 +1409,36 @@ void ProofRun::trace_stage(const zkp_felt* h_trace) {
     draw.ncoef = ncoef;
     draw.out = dt_cc;
     coeffs_drawn = commit_rows(ctx, cm, 0, tlde, n, w, logB, logn, R > 1, "ttree", ttree, T.trace_root,
-                               /*fetch_root=*/false, &draw, nullptr, gu_lazy_on ? &gu_lazy : nullptr);
+                               /*fetch_root=*/host_channel, host_channel ? nullptr : &draw, nullptr,
+                               gu_lazy_on ? &gu_lazy : nullptr);
   }
   troot_d = R > 1 ? ttree.top_d + 8 : ttree.nodes + 8;  // sharded: the device-built top
   // the composition coefficients (drawn on the device from the trace root)
-  if (!coeffs_drawn) launch_dt_draw_coeffs(pf, st, dt_seed, troot_d, o->batching_constraints, ncoef, dt_cc);
+  if (!coeffs_drawn && !host_channel)
+    launch_dt_draw_coeffs(pf, st, dt_seed, troot_d, o->batching_constraints, ncoef, dt_cc);
   ctx->stage_end("1_trace_commit");
 }
 
 // 3-4. constraint evaluation (DefaultConstraintEvaluator) and the composition
 // polynomial + its commitment (CompositionPoly::new + DefaultConstraintCommitment)
 void ProofRun::constraint_stage() {
-  // 3. constraint evaluation (DefaultConstraintEvaluator) with the device-drawn coefficients
+  eval_stage();
+  composition_stage();
+}
+
+// 3. constraint evaluation (DefaultConstraintEvaluator) with the coefficients in
+// dt_cc (device-drawn; a session's caller uploads its own)
+void ProofRun::eval_stage() {
   comp = ctx->buf<felt>("comp", (size_t)(cel ? cel : 1) * n);
   constraint_eval(ctx, air, logn, logB, logce, u0, cel, j0, logBl, cx, twn, dt_cc, dt_aval, tlde, comp, coef, cm);
+}
 
-  // 4. composition polynomial + commitment (CompositionPoly::new +
-  // DefaultConstraintCommitment): per-CE-coset interpolation, exchange of
-  // coefficient slices, ce-point DFT per coefficient, all-gather, coset LDE
+// 4. composition polynomial + commitment (CompositionPoly::new +
+// DefaultConstraintCommitment) from the evaluations in `comp`: per-CE-coset
+// interpolation, exchange of coefficient slices, ce-point DFT per coefficient,
+// all-gather, coset LDE
+void ProofRun::composition_stage() {
+  comp = ctx->buf<felt>("comp", (size_t)(cel ? cel : 1) * n);
   acoef = coef + (size_t)w * n;
   clde = ctx->buf<felt>("clde", (size_t)C * Bl * n);
   bool z_drawn = false;
@@ -1511,16 +1532,17 @@ void ProofRun::constraint_stage() {
     draw.out = dt_zz;
     draw.pw = dt_pw;
     z_drawn = commit_rows(ctx, cm, 0, clde, n, C, logB, logn, R > 1, "ctree", ctree, T.constraint_root,
-                          /*fetch_root=*/false, &draw, derive ? &lc : nullptr);
+                          /*fetch_root=*/host_channel, host_channel ? nullptr : &draw, derive ? &lc : nullptr);
   }
   croot_d = R > 1 ? ctree.top_d + 8 : ctree.nodes + 8;
-  if (!z_drawn) launch_dt_draw_z(pf, st, dt_seed, croot_d, wn_root, logn, dt_zz, dt_pw);
+  if (!z_drawn && !host_channel) launch_dt_draw_z(pf, st, dt_seed, croot_d, wn_root, logn, dt_zz, dt_pw);
   ctx->stage_end("2_constraints_commit");
 }
 
 // 5. OOD frame and the DEEP coefficients (device transcript)
-void ProofRun::ood_stage() {
-  // 5. OOD frame (sharded: every rank holds all coefficients and sums 1/R of each array's blocks)
+// 5a. OOD frame at z = dt_zz[0] (powers in dt_pw; sharded: every rank holds all
+// coefficients and sums 1/R of each array's blocks) and the DEEP denominators
+void ProofRun::ood_values() {
   // the DEEP denominators (x - z)(x - zg) only need z: their batch-inversion
   // phases run on the side stream beside the OOD evaluation and its transcript
   deep_binv = ctx->buf<felt>("binv", ((uint64_t)Bl * n) / 2048 + 1);
@@ -1529,9 +1551,13 @@ void ProofRun::ood_stage() {
   HIP_CHECK(hipStreamWaitEvent(ctx->side, ctx->ev_fork, 0));
   launch_deep_denominators(pf, ctx->side, deep_pm, (uint64_t)Bl * n, dt_zz, dt_pw, deep_binv);
   HIP_CHECK(hipEventRecord(ctx->ev_join, ctx->side));
-  // OOD frame and DEEP coefficients on the device (device transcript); the host
-  // replays both at the FRI round trip
   dv = ood_launch(ctx, coef, w + C, w, logn, dt_pw, cm);  // composition columns at z only
+}
+
+// 5. OOD frame and the DEEP coefficients on the device (device transcript); the
+// host replays both at the FRI round trip
+void ProofRun::ood_stage() {
+  ood_values();
   dgam = ctx->buf<felt>("gamma", w + C);
   dk = ctx->buf<felt>("dt_dk", 4);
   HIP_CHECK(hipMemcpyAsync(dk, dt_zz, 32, hipMemcpyDeviceToDevice, st));
@@ -2025,6 +2051,22 @@ int guarded(zkp_ctx* ctx, F&& f) {
 
 }  // namespace
 
+// a context on `device` with its streams and events (nullptr on failure)
+zkp_ctx* new_ctx(int device) {
+  zkp_ctx* c = new (std::nothrow) zkp_ctx();
+  if (!c) return nullptr;
+  c->device = device;
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&c->copy, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess) {
+    delete c;
+    return nullptr;
+  }
+  return c;
+}
+
 // ====================================================================== C-ABI
 extern "C" {
 
@@ -2037,17 +2079,8 @@ int zkp_ctx_create(int device, zkp_ctx** out) {
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) != hipSuccess) return ZKP_ERR_DEVICE;
   if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) return ZKP_ERR_DEVICE;  // code objects are gfx950-only
-  zkp_ctx* c = new (std::nothrow) zkp_ctx();
-  if (!c) return ZKP_ERR_OOM;
-  c->device = device;
-  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&c->copy, hipStreamNonBlocking) != hipSuccess ||
-      hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess) {
-    delete c;
-    return ZKP_ERR_DEVICE;
-  }
+  zkp_ctx* c = new_ctx(device);
+  if (!c) return ZKP_ERR_DEVICE;
   *out = c;
   return ZKP_OK;
 }
@@ -2055,6 +2088,11 @@ int zkp_ctx_create(int device, zkp_ctx** out) {
 void zkp_ctx_destroy(zkp_ctx* ctx) {
   if (!ctx) return;
   (void)hipSetDevice(ctx->device);
+  for (zkp_ctx* sc : ctx->session_pool) {  // idle session contexts (stage sessions)
+    drain_streams(sc);
+    delete sc;
+  }
+  ctx->session_pool.clear();
   drain_streams(ctx);
   delete ctx;
 }
@@ -2305,16 +2343,16 @@ int zkp_grind(zkp_ctx* ctx, const uint8_t seed[32], uint32_t bits, uint64_t* non
     for (int i = 0; i < 8; i++)
       sw[i] = (uint32_t)seed[4 * i] | ((uint32_t)seed[4 * i + 1] << 8) | ((uint32_t)seed[4 * i + 2] << 16) |
               ((uint32_t)seed[4 * i + 3] << 24);
+    // one launch to the minimum nonce (k_grind_all), as zkp_prove's device query tail
     unsigned long long* dres = ctx->buf<unsigned long long>("grind_res", 1);
-    const uint64_t chunk = 1ull << 22;
-    for (uint64_t base = 1;; base += chunk) {
-      unsigned long long init = ~0ull, res;
-      ctx->upload(dres, &init, 8);
-      launch_grind(ctx->prof, ctx->stream, sw, nullptr, base, chunk, bits, dres);
-      ctx->download(&res, dres, 8);
-      if (res != ~0ull) { *nonce = res; break; }
-      if (base > (1ull << 40)) return (int)ZKP_ERR_NONCE;
-    }
+    uint32_t* dseed = ctx->buf<uint32_t>("grind_seed", 8);
+    ctx->upload(dseed, sw, 32);
+    HIP_CHECK(hipMemsetAsync(dres, 0xff, 8, ctx->stream));
+    launch_grind_all(ctx->prof, ctx->stream, dseed, 1, 1ull << 40, bits, dres);
+    unsigned long long res;
+    ctx->download(&res, dres, 8);
+    if (res == ~0ull) return (int)ZKP_ERR_NONCE;
+    *nonce = res;
     ctx->collect_prof();
     return 0;
   });
@@ -2426,32 +2464,53 @@ int zkp_build_mimc_trace(const uint8_t seed[16], uint64_t n, zkp_felt* out) {
 // ====================================================================== stage sessions
 // The stage entry points of include/zkp.h: one proof's
 // device-resident state, driven stage by stage by a caller that keeps its own
-// Fiat-Shamir channel (a winter-prover 0.12 fork keeping `Prover::prove`).
-// Same kernels as zkp_prove; the coin draws come from the caller instead of
-// the device transcript. World 1 (one GPU).
+// Fiat-Shamir channel (a winter-prover 0.12 fork keeping `Prover::prove`). The
+// stages are zkp_prove's own (ProofRun in host-channel mode: grouped upload,
+// GlobalUpdate column pairing, coefficient-form linear evaluation, the derived
+// last composition column, coefficient-form DEEP for wide traces), with the coin
+// draws coming from the caller. The shortcuts' device checks are read before the
+// stage returns its root: a failed check redoes that stage without the shortcut,
+// so every returned value is the one winterfell computes. World 1 (one GPU).
 struct zkp_session {
-  zkp_ctx* ctx = nullptr;
-  AirDesc air;
+  zkp_ctx* parent = nullptr;  // the caller's context (errors, kernel statistics)
+  zkp_ctx* ctx = nullptr;     // this session's context (from the parent's pool)
   zkp_proof_options o{};
+  std::unique_ptr<ProofRun> run;
+  int air_id = 0;
+  std::vector<zkp_felt> pub;
   uint32_t w = 0, B = 0, ce = 0, C = 0, F = 16, L = 0;
-  uint32_t logn = 0, logB = 0, logce = 0, logN = 0;
+  uint32_t logn = 0, logB = 0, logN = 0;
   uint64_t n = 0, N = 0;
   int stage = 0;  // 1 trace committed, 2 evaluated, 3 composition committed, 4 OOD, 5 DEEP/FRI done
-  std::string pfx;
-  TreeShard ttree, ctree;
   std::vector<FriLayer> layers;
   felt z{}, zg{};
   std::vector<felt> ood;  // [2a + {0,1}]: array a (trace columns, then composition columns) at z, zg
 
-  template <typename T>
-  T* buf(const char* name, size_t count) { return ctx->buf<T>(pfx + name, count); }
-  felt* get(const char* name) { return reinterpret_cast<felt*>(ctx->bufs[pfx + name].p); }
   void begin(int need) {
     if (stage != need) throw ZkpFail{ZKP_ERR_ARGUMENT, "stage entry point called out of order"};
     HIP_CHECK(hipSetDevice(ctx->device));
     ctx->sync();
     ctx->ring_reset();
   }
+  // a fresh ProofRun over the session's trace buffer, set up for host-channel stages
+  void start_run(bool shortcuts) {
+    run.reset(new ProofRun(ctx, ctx->self_comm(), &o));
+    run->host_channel = true;
+    run->allow_shortcuts = shortcuts;
+    uint8_t* dummy = nullptr;
+    uint64_t dlen = 0;
+    felt* d = ctx->buf<felt>("trace_in", (size_t)w * n);
+    const int rc = run->init(air_id, d, w, n, pub.data(), pub.size(), &dummy, &dlen);
+    if (rc) throw ZkpFail{rc, "session: proof shape"};
+    run->setup();
+  }
+};
+
+// the host channel of include/zkp.h (zkp_channel_*)
+struct zkp_channel {
+  Coin coin;
+  uint64_t lde_size = 0;
+  uint32_t num_queries = 0;
 };
 
 namespace {
@@ -2459,13 +2518,28 @@ namespace {
 template <typename Fn>
 int session_guard(zkp_session* s, Fn&& f) {
   if (!s) return ZKP_ERR_ARGUMENT;
-  return guarded(s->ctx, [&] {
-    s->ctx->err.clear();
-    int rc = f();
-    s->ctx->collect_prof();
-    return rc;
+  zkp_ctx* sc = s->ctx;
+  sc->prof.enabled = s->parent->prof.enabled;
+  sc->prof.only = s->parent->prof.only;
+  const int rc = guarded(sc, [&] {
+    sc->err.clear();
+    int r = f();
+    sc->collect_prof();
+    return r;
   });
+  // the caller reads errors and kernel statistics from its own context
+  s->parent->err = sc->err;
+  for (auto& kv : sc->stats) {
+    auto& d = s->parent->stats[kv.first];
+    d.launches += kv.second.launches;
+    d.ms += kv.second.ms;
+    d.bytes += kv.second.bytes;
+  }
+  sc->stats.clear();
+  return rc;
 }
+
+void upload_felts(zkp_ctx* ctx, felt* d, const std::vector<felt>& h) { ctx->upload(d, h.data(), h.size() * 16); }
 
 }  // namespace
 
@@ -2482,21 +2556,31 @@ int zkp_session_create(zkp_ctx* ctx, zkp_air_id air_id, uint32_t width, uint64_t
     if (n_pub && !pub_elems) return (int)ZKP_ERR_ARGUMENT;
     std::vector<felt> pub(n_pub);
     for (uint64_t i = 0; i < n_pub; i++) pub[i] = make(pub_elems[i].lo, pub_elems[i].hi);
-    auto s = std::make_unique<zkp_session>();
-    rc = build_air(s->air, air_id, width, n, pub);
+    AirDesc air;
+    rc = build_air(air, air_id, width, n, pub);
     if (rc) return rc;
-    s->ctx = ctx;
+    auto s = std::make_unique<zkp_session>();
+    s->parent = ctx;
     s->o = *o;
+    s->air_id = air_id;
+    s->pub.assign(pub_elems, pub_elems + n_pub);
     s->w = width; s->n = n; s->B = o->blowup_factor; s->F = o->fri_folding_factor;
-    s->ce = s->air.ce_blowup(); s->C = s->air.comp_cols();
+    s->ce = air.ce_blowup(); s->C = air.comp_cols();
     if (s->B < s->ce) return (int)ZKP_ERR_INVALID_OPTIONS;
     if (s->ce > 16 || s->C > s->ce) return (int)ZKP_ERR_UNSUPPORTED_AIR;
-    s->logn = ilog2(n); s->logB = ilog2(s->B); s->logce = ilog2(s->ce); s->logN = s->logn + s->logB;
+    s->logn = ilog2(n); s->logB = ilog2(s->B); s->logN = s->logn + s->logB;
     s->N = n << s->logB;
     if (s->logN > MAX_LOG_DOMAIN || s->logn > MAX_LOG_TRACE) return (int)ZKP_ERR_TRACE_SHAPE;
     uint64_t D = s->N, maxrem = (uint64_t)(o->fri_remainder_max_degree + 1) * s->B;
     while (D > maxrem) { D /= s->F; s->L++; }
-    s->pfx = "sess" + std::to_string(ctx->next_session++) + "_";
+    HIP_CHECK(hipSetDevice(ctx->device));
+    if (!ctx->session_pool.empty()) {
+      s->ctx = ctx->session_pool.back();
+      ctx->session_pool.pop_back();
+    } else {
+      s->ctx = new_ctx(ctx->device);
+      if (!s->ctx) return (int)ZKP_ERR_DEVICE;
+    }
     *out = s.release();
     return 0;
   });
@@ -2504,11 +2588,13 @@ int zkp_session_create(zkp_ctx* ctx, zkp_air_id air_id, uint32_t width, uint64_t
 
 void zkp_session_destroy(zkp_session* s) {
   if (!s) return;
-  (void)guarded(s->ctx, [&] {
-    HIP_CHECK(hipSetDevice(s->ctx->device));
-    s->ctx->drop(s->pfx);
-    return 0;
-  });
+  s->run.reset();
+  if (s->ctx) {
+    (void)hipSetDevice(s->ctx->device);
+    drain_streams(s->ctx);
+    s->ctx->err.clear();
+    s->parent->session_pool.push_back(s->ctx);  // buffers and domain tables kept for the next session
+  }
   delete s;
 }
 
@@ -2520,69 +2606,59 @@ int zkp_session_shape(const zkp_session* s, uint32_t* ce, uint32_t* num_columns,
   return ZKP_OK;
 }
 
+// ≙ Prover::new_trace_lde + the trace commitment (DefaultTraceLde::new)
 int zkp_session_trace_lde(zkp_session* s, const zkp_felt* trace_cols, uint8_t root[32]) {
   return session_guard(s, [&] {
     if (!trace_cols || !root) return (int)ZKP_ERR_ARGUMENT;
     s->begin(0);
-    zkp_ctx* ctx = s->ctx;
-    const uint64_t n = s->n;
-    felt* d = s->buf<felt>("trace", (size_t)s->w * n);
-    ctx->upload(d, trace_cols, (size_t)s->w * n * 16);
-    ctx->ensure_coset(s->logn, s->logB, s->logce);
-    felt* coef = s->buf<felt>("coef", (size_t)(s->w + s->C) * n);
-    felt* tlde = s->buf<felt>("tlde", (size_t)s->w * s->N);
-    NttBatch ib{d, coef, nullptr, n, n, 1, 1, s->w};
-    launch_ntt(ctx->prof, ctx->stream, ib, s->logn, false, ctx->itws(s->logN), s->logN);
-    NttBatch lb{coef, tlde, ctx->S(s->logn, s->logB), n, n, s->B, s->B, s->w * s->B};
-    launch_ntt(ctx->prof, ctx->stream, lb, s->logn, true, ctx->tws(s->logN), s->logN);
-    commit_rows(ctx, ctx->self_comm(), 0, tlde, n, s->w, s->logB, s->logn, false, s->pfx + "ttree", s->ttree, root);
+    s->start_run(true);
+    s->run->trace_stage(trace_cols);
+    // GlobalUpdate pairing: the check of every row (the late host columns joined)
+    // before the root is returned; a failed check extends every column instead
+    if (s->run->pair_failed()) {
+      s->start_run(false);
+      s->run->trace_stage(s->run->h_partial ? trace_cols : nullptr);
+    }
+    memcpy(root, s->run->T.trace_root, 32);
     s->stage = 1;
     return 0;
   });
 }
 
+// ≙ new_evaluator(..).evaluate: the caller's composition coefficients
 int zkp_eval_constraints(zkp_session* s, const zkp_felt* coeffs, uint32_t n_coeffs, zkp_felt* evals_out) {
   return session_guard(s, [&] {
     if (!coeffs) return (int)ZKP_ERR_ARGUMENT;
     s->begin(1);
-    zkp_ctx* ctx = s->ctx;
-    const AirDesc& air = s->air;
-    if (n_coeffs != air.num_t + air.a_col.size()) return (int)ZKP_ERR_ARGUMENT;
-    felt* dcc = s->buf<felt>("cc", n_coeffs);
-    ctx->upload(dcc, coeffs, (size_t)n_coeffs * 16);
-    felt* daval = s->buf<felt>("aval", air.a_val.size());
-    ctx->upload(daval, air.a_val.data(), air.a_val.size() * 16);
-    felt* cx = coset_points(ctx, s->logn, s->logB, s->logce);
-    const felt* twn = ctx->tws(s->logN) + ((1ull << (s->logn - 1)) - 1);
-    felt* comp = s->buf<felt>("comp", (size_t)s->ce * s->n);
-    constraint_eval(ctx, air, s->logn, s->logB, s->logce, 0, s->ce, 0, s->logB, cx, twn, dcc, daval, s->get("tlde"),
-                    comp, s->get("coef"));
+    ProofRun& r = *s->run;
+    if (n_coeffs != r.ncoef) return (int)ZKP_ERR_ARGUMENT;
+    s->ctx->upload(r.dt_cc, coeffs, (size_t)n_coeffs * 16);
+    r.eval_stage();
     if (evals_out) {  // CE-coset-major on the device -> natural CE domain order
       std::vector<felt> h((size_t)s->ce * s->n);
-      ctx->download(h.data(), comp, h.size() * 16);
+      s->ctx->download(h.data(), r.comp, h.size() * 16);
       for (uint32_t u = 0; u < s->ce; u++)
         for (uint64_t t = 0; t < s->n; t++) {
           const felt v = h[(size_t)u * s->n + t];
           evals_out[u + (size_t)s->ce * t] = zkp_felt{v.lo, v.hi};
         }
     }
-    ctx->sync();
+    s->ctx->sync();
     s->stage = 2;
     return 0;
   });
 }
 
+// ≙ build_constraint_commitment (CompositionPoly::new + DefaultConstraintCommitment);
+// evals (nullable): the caller's own evaluations in natural CE-domain order
 int zkp_composition_commit(zkp_session* s, const zkp_felt* evals, uint8_t root[32], uint32_t* num_columns) {
   return session_guard(s, [&] {
     if (!root) return (int)ZKP_ERR_ARGUMENT;
     if (evals && s->stage == 1) s->stage = 2;  // caller-evaluated constraints (natural CE order)
     s->begin(2);
-    zkp_ctx* ctx = s->ctx;
-    Prof& pf = ctx->prof;
-    hipStream_t st = ctx->stream;
+    ProofRun& r = *s->run;
     const uint64_t n = s->n;
-    const uint32_t ce = s->ce, C = s->C;
-    felt* comp = s->buf<felt>("comp", (size_t)ce * n);
+    const uint32_t ce = s->ce;
     if (evals) {
       std::vector<felt> h((size_t)ce * n);
       for (uint32_t u = 0; u < ce; u++)
@@ -2591,28 +2667,17 @@ int zkp_composition_commit(zkp_session* s, const zkp_felt* evals, uint8_t root[3
           h[(size_t)u * n + t] = make(v.lo, v.hi);
           if (ge_p(h[(size_t)u * n + t])) throw ZkpFail{ZKP_ERR_ARGUMENT, "non-canonical evaluation"};
         }
-      ctx->upload(comp, h.data(), h.size() * 16);
+      upload_felts(s->ctx, s->ctx->buf<felt>("comp", (size_t)ce * n), h);
     }
-    NttBatch ib{comp, comp, nullptr, n, n, 1, 1, ce};
-    launch_ntt(pf, st, ib, s->logn, false, ctx->itws(s->logN), s->logN);
-    const std::string dkey = "comp_dft_" + std::to_string(s->logn) + "_" + std::to_string(s->logce) + "_" +
-                             std::to_string(C) + "_1_" + std::to_string(ce);
-    felt* dcoefs = ctx->buf<felt>(dkey + "_coefs", (size_t)C + ce / 2);
-    uint32_t* dblk = ctx->buf<uint32_t>(dkey + "_blk", ce);
-    if (!ctx->have_cached(dkey)) {  // world 1: blk[u] = u (same table as zkp_prove's)
-      const std::vector<felt> dc = comp_dft_consts(n, s->logce, C);
-      std::vector<uint32_t> blk(ce);
-      for (uint32_t u = 0; u < ce; u++) blk[u] = u;
-      ctx->upload(dcoefs, dc.data(), dc.size() * 16);
-      ctx->upload(dblk, blk.data(), blk.size() * 4);
+    r.composition_stage();
+    // the derived last column holds only if the dropped segments are zero: else
+    // the composition is committed again with the column extended
+    if (r.lastcol_failed()) {
+      r.allow_shortcuts = false;
+      r.composition_stage();
     }
-    felt* acoef = s->get("coef") + (size_t)s->w * n;
-    launch_comp_dft(pf, st, comp, dblk, ctx->Si(s->logn, s->logB, s->logce), dcoefs, ce, C, s->logn, 0, n, acoef);
-    felt* clde = s->buf<felt>("clde", (size_t)C * s->N);
-    NttBatch lb{acoef, clde, ctx->S(s->logn, s->logB), n, n, s->B, s->B, C * s->B};
-    launch_ntt(pf, st, lb, s->logn, true, ctx->tws(s->logN), s->logN);
-    commit_rows(ctx, ctx->self_comm(), 0, clde, n, C, s->logB, s->logn, false, s->pfx + "ctree", s->ctree, root);
-    if (num_columns) *num_columns = C;
+    memcpy(root, r.T.constraint_root, 32);
+    if (num_columns) *num_columns = s->C;
     s->stage = 3;
     return 0;
   });
@@ -2622,18 +2687,18 @@ int zkp_ood_frame(zkp_session* s, zkp_felt zf, zkp_felt* trace_ood, zkp_felt* co
   return session_guard(s, [&] {
     if (!trace_ood || !comp_ood) return (int)ZKP_ERR_ARGUMENT;
     s->begin(3);
-    zkp_ctx* ctx = s->ctx;
+    ProofRun& r = *s->run;
     s->z = make(zf.lo, zf.hi);
     if (ge_p(s->z)) return (int)ZKP_ERR_ARGUMENT;
     s->zg = mul(s->z, root_of_unity(s->logn));
-    std::vector<felt> pw(2 * (size_t)s->logn);
+    std::vector<felt> pw(2 * (size_t)s->logn), zz = {s->z, s->zg};
     felt a = s->z, b = s->zg;
     for (uint32_t l = 0; l < s->logn; l++) { pw[l] = a; pw[s->logn + l] = b; a = sqr(a); b = sqr(b); }
-    felt* dpw = s->buf<felt>("pw", pw.size());
-    ctx->upload(dpw, pw.data(), pw.size() * 16);
-    felt* dv = ood_launch(ctx, s->get("coef"), s->w + s->C, s->w, s->logn, dpw);
+    upload_felts(s->ctx, r.dt_pw, pw);
+    upload_felts(s->ctx, r.dt_zz, zz);
+    r.ood_values();
     s->ood.resize(2 * (size_t)(s->w + s->C));
-    ctx->download(s->ood.data(), dv, s->ood.size() * 16);
+    s->ctx->download(s->ood.data(), r.dv, s->ood.size() * 16);
     for (uint32_t c = 0; c < s->w; c++) {
       trace_ood[c] = zkp_felt{s->ood[2 * c].lo, s->ood[2 * c].hi};
       trace_ood[s->w + c] = zkp_felt{s->ood[2 * c + 1].lo, s->ood[2 * c + 1].hi};
@@ -2650,6 +2715,7 @@ int zkp_deep_fri(zkp_session* s, const zkp_felt* deep_coeffs, zkp_fri_channel ch
     if (!deep_coeffs || !channel || !remainder_len || !remainder_commitment) return (int)ZKP_ERR_ARGUMENT;
     s->begin(4);
     zkp_ctx* ctx = s->ctx;
+    ProofRun& r = *s->run;
     Prof& pf = ctx->prof;
     hipStream_t st = ctx->stream;
     const uint32_t w = s->w, C = s->C, B = s->B, F = s->F;
@@ -2665,31 +2731,19 @@ int zkp_deep_fri(zkp_session* s, const zkp_felt* deep_coeffs, zkp_fri_channel ch
     }
     for (uint32_t h = 0; h < C; h++) kz = add(kz, mul(gam[w + h], s->ood[2 * (w + h)]));
     dkh[0] = s->z; dkh[1] = s->zg; dkh[2] = kz; dkh[3] = kzg;
-    felt* dgam = s->buf<felt>("gamma", w + C);
-    felt* dk = s->buf<felt>("dk", 4);
-    ctx->upload(dgam, gam.data(), gam.size() * 16);
-    ctx->upload(dk, dkh.data(), 64);
-    felt* cx = coset_points(ctx, s->logn, s->logB, s->logce);
-    const felt* twn = ctx->tws(s->logN) + ((1ull << (s->logn - 1)) - 1);
-    const PointMap pm{cx, twn, s->logn};
-    felt* binv = s->buf<felt>("binv", s->N / 2048 + 1);
-    launch_deep_denominators(pf, st, pm, s->N, dk, s->get("pw"), binv);
-    felt* deep = s->buf<felt>("deep", s->N);
-    DeepArgs da;
-    da.w = w; da.C = C; da.logB = s->logB; da.logn = s->logn; da.logN = s->logN;
-    da.j0 = 0; da.logBl = s->logB;
-    da.tlde = s->get("tlde"); da.clde = s->get("clde"); da.gamma = dgam; da.dk = dk; da.g = g;
-    da.pm = pm;
-    da.binv = binv;
-    deep_evaluations(ctx, ctx->self_comm(), st, da, s->get("coef"), n, ctx->S(s->logn, s->logB), s->logN, deep);
+    r.dgam = ctx->buf<felt>("gamma", w + C);
+    r.dk = ctx->buf<felt>("dt_dk", 4);
+    upload_felts(ctx, r.dgam, gam);
+    upload_felts(ctx, r.dk, dkh);
+    r.deep_stage();
     // FriProver::build_layers: commit each layer, the caller's channel returns alpha, fold
     s->layers.assign(s->L + 1, FriLayer{});
     uint64_t tot = 0, D = s->N;
     for (uint32_t l = 0; l < s->L; l++) { tot += D / F; D /= F; }
-    felt* fe = s->buf<felt>("fri_evals", tot + 1);
-    felt* alphas = s->buf<felt>("alphas", s->L + 1);
+    felt* fe = ctx->buf<felt>("fri_evals", tot + 1);
+    felt* alphas = ctx->buf<felt>("alphas", s->L + 1);
     const felt* deps = fold_constants(ctx);
-    felt* E = deep;
+    felt* E = r.deep;
     uint64_t m = n, eo = 0;
     felt off = g;
     D = s->N;
@@ -2698,7 +2752,7 @@ int zkp_deep_fri(zkp_session* s, const zkp_felt* deep_coeffs, zkp_fri_channel ch
       FriLayer& ly = s->layers[l];
       ly.E = E; ly.m = m; ly.Bc = B; ly.jc = 0; ly.sharded = false;
       uint8_t root[32];
-      commit_rows(ctx, ctx->self_comm(), 1, E, 0, F, s->logB, ilog2(m16), false, s->pfx + "ftree_" + std::to_string(l),
+      commit_rows(ctx, ctx->self_comm(), 1, E, 0, F, s->logB, ilog2(m16), false, "ftree_" + std::to_string(l),
                   ly.tree, root);
       zkp_felt af{0, 0};
       if (channel(user, l, root, &af) != 0) throw ZkpFail{ZKP_ERR_ARGUMENT, "FRI channel callback failed"};
@@ -2740,9 +2794,16 @@ int zkp_query(zkp_session* s, const uint64_t* positions, uint64_t n_positions, u
     for (uint64_t i = 0; i < n_positions; i++)
       if (pos[i] >= s->N || (i && pos[i] <= pos[i - 1])) return (int)ZKP_ERR_ARGUMENT;  // sorted, unique, in range
     zkp_ctx* ctx = s->ctx;
+    ProofRun& r = *s->run;
+    if (r.gu_lazy_on) {  // the lazy paired columns of the queried rows
+      uint64_t* dq = ctx->buf<uint64_t>("gu_fill_pos", pos.size());
+      ctx->upload(dq, pos.data(), pos.size() * 8);
+      launch_gu_fill(ctx->prof, ctx->stream, r.tlde, s->w, s->logn, s->logB, 0, s->logB, dq, (uint32_t)pos.size(),
+                     r.gu_lazy);
+    }
     Openings op;
-    gather_openings(ctx, ctx->self_comm(), pos, s->n, s->logB, 0, s->get("tlde"), s->w, s->ttree, s->get("clde"), s->C,
-                    s->ctree, s->layers, s->L, s->F, op);
+    gather_openings(ctx, ctx->self_comm(), pos, s->n, s->logB, 0, r.tlde, s->w, r.ttree, r.clde, s->C, r.ctree,
+                    s->layers, s->L, s->F, op);
     Writer wr;
     wr.u8(1);  // one trace segment
     op.write_commitment_queries(wr);
@@ -2756,6 +2817,86 @@ int zkp_query(zkp_session* s, const uint64_t* positions, uint64_t n_positions, u
     s->stage = 5;  // queries may be asked again (e.g. after a re-grind)
     return 0;
   });
+}
+
+// ---- host channel (≙ ProverChannel over DefaultRandomCoin<Blake3_256>)
+int zkp_channel_create(zkp_air_id air_id, uint32_t width, uint64_t n, const zkp_felt* pub_elems, uint64_t n_pub,
+                       const zkp_proof_options* o, zkp_channel** out) {
+  if (!out) return ZKP_ERR_ARGUMENT;
+  *out = nullptr;
+  try {
+    int rc = check_options(o);
+    if (rc) return rc;
+    if (n < 8 || (n & (n - 1)) || width == 0 || width > 255) return ZKP_ERR_TRACE_SHAPE;
+    if (n_pub && !pub_elems) return ZKP_ERR_ARGUMENT;
+    std::vector<felt> pub(n_pub);
+    for (uint64_t i = 0; i < n_pub; i++) pub[i] = make(pub_elems[i].lo, pub_elems[i].hi);
+    AirDesc air;
+    rc = build_air(air, air_id, width, n, pub);
+    if (rc) return rc;
+    auto ch = std::make_unique<zkp_channel>();
+    std::vector<felt> se = context_elements(air, o);
+    se.insert(se.end(), pub.begin(), pub.end());
+    ch->coin.init(se);
+    ch->lde_size = n * o->blowup_factor;
+    ch->num_queries = o->num_queries;
+    *out = ch.release();
+    return ZKP_OK;
+  } catch (const ZkpFail& e) {
+    return e.code;
+  } catch (...) {
+    return ZKP_ERR_OOM;
+  }
+}
+
+void zkp_channel_destroy(zkp_channel* ch) { delete ch; }
+
+int zkp_channel_commit(zkp_channel* ch, const uint8_t root[32]) {
+  if (!ch || !root) return ZKP_ERR_ARGUMENT;
+  ch->coin.reseed(root);
+  return ZKP_OK;
+}
+
+int zkp_channel_commit_felts(zkp_channel* ch, const zkp_felt* els, uint64_t n) {
+  if (!ch || (n && !els)) return ZKP_ERR_ARGUMENT;
+  std::vector<felt> v(n);
+  for (uint64_t i = 0; i < n; i++) v[i] = make(els[i].lo, els[i].hi);
+  uint8_t d[32];
+  hash_elements(v.data(), v.size(), d);
+  ch->coin.reseed(d);
+  return ZKP_OK;
+}
+
+int zkp_channel_draw(zkp_channel* ch, uint32_t method, uint32_t count, zkp_felt* out) {
+  if (!ch || !out || method > ZKP_BATCHING_HORNER) return ZKP_ERR_ARGUMENT;
+  try {
+    if (count == 0) {
+      const felt v = ch->coin.draw();
+      out[0] = zkp_felt{v.lo, v.hi};
+      return ZKP_OK;
+    }
+    const std::vector<felt> v = draw_coeffs(ch->coin, method, count);
+    for (uint32_t i = 0; i < count; i++) out[i] = zkp_felt{v[i].lo, v[i].hi};
+    return ZKP_OK;
+  } catch (const ZkpFail& e) {
+    return e.code;
+  }
+}
+
+int zkp_channel_seed(const zkp_channel* ch, uint8_t seed[32]) {
+  if (!ch || !seed) return ZKP_ERR_ARGUMENT;
+  memcpy(seed, ch->coin.seed, 32);
+  return ZKP_OK;
+}
+
+int zkp_channel_query_positions(zkp_channel* ch, uint64_t nonce, uint64_t* out, uint32_t* n_unique) {
+  if (!ch || !out || !n_unique) return ZKP_ERR_ARGUMENT;
+  std::vector<uint64_t> pos = ch->coin.draw_integers(ch->num_queries, ch->lde_size, nonce);
+  std::sort(pos.begin(), pos.end());
+  pos.erase(std::unique(pos.begin(), pos.end()), pos.end());
+  for (size_t i = 0; i < pos.size(); i++) out[i] = pos[i];
+  *n_unique = (uint32_t)pos.size();
+  return ZKP_OK;
 }
 
 }  // extern "C"
