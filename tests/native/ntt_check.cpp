@@ -1,0 +1,177 @@
+// ntt_check.cpp — correctness of launch_ntt (csrc/ntt.hip, linked directly) on
+// inputs that drive the deferred-check rounds into their exact recomputation
+// (TEST ONLY; run by tests/test_gpu_ntt.py). The NTT rounds take every product
+// and sum as canonical and redo a round with the exact forms when a lane saw a
+// carry past 2^128 or a top limb 0xffffffff. Random data reaches
+// that branch about once per 2^26 operations, so the parity tests never do;
+// here the inputs put p - 1 against small values so the first stages' sums land
+// in [p, 2^128) in every lane (dense) or in one lane of many (sparse), for the DIF
+// (natural in, bit-reversed out) and DIT (bit-reversed in, natural out, with and
+// without the coset scale) passes, 2^11 .. 2^18, several batches. Every output
+// is compared with a naive O(n^2) host DFT (2^11) or the host radix-2 NTT.
+// Prints one line per case and exits non-zero on any mismatch.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../zk_stark_project_amd/csrc/zkp_internal.hpp"
+#include "../../zk_stark_project_amd/csrc/host_stark.hpp"
+
+using namespace fp;
+using namespace zkh;
+
+// the product's Prof and launch_fail live in kernels.hip / prover.cpp
+hipEvent_t Prof::get_event() { return nullptr; }
+void Prof::begin(const char*, hipStream_t, double) {}
+void Prof::end(hipStream_t) {}
+void launch_fail(int code, const char* what) { throw std::runtime_error(std::string(what) + " " + std::to_string(code)); }
+
+#define CK(x)                                                                   \
+  do {                                                                          \
+    hipError_t e_ = (x);                                                        \
+    if (e_ != hipSuccess) {                                                     \
+      fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e_));                   \
+      exit(2);                                                                  \
+    }                                                                           \
+  } while (0)
+
+static uint64_t rs = 0x243F6A8885A308D3ull;
+static uint64_t rnd() {
+  rs ^= rs << 13; rs ^= rs >> 7; rs ^= rs << 17;
+  return rs;
+}
+static felt rand_felt() {
+  for (;;) {
+    felt v = make(rnd(), rnd());
+    if (!ge_p(v)) return v;
+  }
+}
+static uint32_t rev(uint32_t x, uint32_t bits) {
+  uint32_t r = 0;
+  for (uint32_t i = 0; i < bits; i++) r |= ((x >> i) & 1u) << (bits - 1 - i);
+  return r;
+}
+
+// stage-major table of a 2^logN domain: level t at [2^t - 1, 2^(t+1) - 1) holds w_{2^(t+1)}^j
+static std::vector<felt> stage_table(uint32_t logN, bool inverse) {
+  std::vector<felt> t((size_t)1 << logN);
+  for (uint32_t lev = 0; lev < logN; lev++) {
+    felt w = root_of_unity(lev + 1);
+    if (inverse) w = inv(w);
+    felt acc = one();
+    for (uint64_t j = 0; j < (1ull << lev); j++) {
+      t[((1ull << lev) - 1) + j] = acc;
+      acc = mul(acc, w);
+    }
+  }
+  return t;
+}
+
+// host transforms: DIT = bit-reversed in -> natural out, sum x_i w^(ik);
+// DIF = natural in -> bit-reversed out, sum x_i w^(-ik)
+static std::vector<felt> host_ref(const std::vector<felt>& in, uint32_t logn, bool dit) {
+  const uint64_t n = 1ull << logn;
+  std::vector<felt> nat(n), out(n);
+  if (dit) {
+    for (uint64_t i = 0; i < n; i++) nat[i] = in[rev((uint32_t)i, logn)];
+  } else {
+    nat = in;
+  }
+  felt w = root_of_unity(logn);
+  if (!dit) w = inv(w);
+  // radix-2 recursive-free NTT on natural order (host_ntt from host_stark.hpp)
+  std::vector<felt> v = nat;
+  host_ntt(v, w);
+  if (dit) return v;
+  for (uint64_t k = 0; k < n; k++) out[rev((uint32_t)k, logn)] = v[k];
+  return out;
+}
+
+static std::vector<felt> naive(const std::vector<felt>& in, uint32_t logn, bool dit) {
+  const uint64_t n = 1ull << logn;
+  felt w = root_of_unity(logn);
+  if (!dit) w = inv(w);
+  std::vector<felt> out(n);
+  for (uint64_t k = 0; k < n; k++) {
+    felt acc = zero(), wk = pow_u64(w, k), p = one();
+    for (uint64_t i = 0; i < n; i++) {
+      const felt xi = dit ? in[rev((uint32_t)i, logn)] : in[i];
+      acc = add(acc, mul(xi, p));
+      p = mul(p, wk);
+    }
+    if (dit) out[k] = acc;
+    else out[rev((uint32_t)k, logn)] = acc;
+  }
+  return out;
+}
+
+int main() {
+  setvbuf(stdout, NULL, _IONBF, 0);
+  hipStream_t st;
+  CK(hipStreamCreate(&st));
+  Prof pf;
+  const felt pm1 = make(0xffffd30000000000ull, 0xffffffffffffffffull);  // p - 1
+  int bad = 0, cases = 0;
+  for (uint32_t logn : {11u, 13u, 18u}) {
+    const uint64_t n = 1ull << logn;
+    const uint32_t logN = logn + 1;
+    const std::vector<felt> twf = stage_table(logN, false), twi = stage_table(logN, true);
+    felt *dtf, *dti;
+    CK(hipMalloc(&dtf, twf.size() * 16));
+    CK(hipMalloc(&dti, twi.size() * 16));
+    CK(hipMemcpy(dtf, twf.data(), twf.size() * 16, hipMemcpyHostToDevice));
+    CK(hipMemcpy(dti, twi.data(), twi.size() * 16, hipMemcpyHostToDevice));
+    for (int dit = 0; dit < 2; dit++)
+      for (int pattern = 0; pattern < 3; pattern++)
+        for (int scaled = 0; scaled < (dit ? 2 : 1); scaled++) {
+          const uint32_t batches = 3;
+          std::vector<felt> h((size_t)batches * n), S(scaled ? (size_t)2 * n : 0);
+          for (uint32_t b = 0; b < batches; b++)
+            for (uint64_t i = 0; i < n; i++) {
+              felt v = rand_felt();
+              // the first stage's partner of i: i + n/2 (DIF), i ^ 1 in storage order (DIT)
+              const bool lo_half = dit ? (i & 1) == 0 : i < n / 2;
+              if (pattern == 0) v = lo_half ? pm1 : make(rnd() & 0xffffffffull, 0);            // dense: every lane
+              if (pattern == 1 && (i % 97) < 2) v = lo_half ? pm1 : make(rnd() & 0xffff, 0);   // sparse lanes
+              if (pattern == 2 && (i % 5) == 0) v = sub(pm1, make(rnd() & 0xff, 0));          // near p, random partners
+              h[(size_t)b * n + i] = v;
+            }
+          for (auto& x : S) x = (rnd() & 3) ? rand_felt() : one();  // scale 1 keeps the rare sums
+          felt *d, *ds = nullptr;
+          CK(hipMalloc(&d, h.size() * 16));
+          CK(hipMemcpy(d, h.data(), h.size() * 16, hipMemcpyHostToDevice));
+          if (scaled) {
+            CK(hipMalloc(&ds, S.size() * 16));
+            CK(hipMemcpy(ds, S.data(), S.size() * 16, hipMemcpyHostToDevice));
+          }
+          NttBatch nb{d, d, ds, n, n, 1, scaled ? 2u : 1u, batches};
+          launch_ntt(pf, st, nb, logn, dit != 0, dit ? dtf : dti, logN);
+          CK(hipStreamSynchronize(st));
+          std::vector<felt> g(h.size());
+          CK(hipMemcpy(g.data(), d, g.size() * 16, hipMemcpyDeviceToHost));
+          int mism = 0;
+          for (uint32_t b = 0; b < batches; b++) {
+            std::vector<felt> in(h.begin() + (size_t)b * n, h.begin() + (size_t)(b + 1) * n);
+            if (scaled)
+              for (uint64_t i = 0; i < n; i++) in[i] = mul(in[i], S[(size_t)(b % 2) * n + i]);
+            const std::vector<felt> want = logn == 11 ? naive(in, logn, dit != 0) : host_ref(in, logn, dit != 0);
+            for (uint64_t i = 0; i < n; i++)
+              if (!eq(want[i], g[(size_t)b * n + i])) mism++;
+          }
+          cases++;
+          if (mism) bad++;
+          printf("n=2^%u %s pattern=%d scale=%d batches=%u: %s\n", logn, dit ? "DIT" : "DIF", pattern, scaled, batches,
+                 mism ? "MISMATCH" : "ok");
+          CK(hipFree(d));
+          if (ds) CK(hipFree(ds));
+        }
+    CK(hipFree(dtf));
+    CK(hipFree(dti));
+  }
+  printf("%d cases, %d mismatching\n", cases, bad);
+  return bad ? 1 : 0;
+}

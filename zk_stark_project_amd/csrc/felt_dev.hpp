@@ -239,8 +239,10 @@ __device__ __forceinline__ void mul256(L4 x, L4 y, uint32_t r[8]) {
   r[7] = (uint32_t)(acc >> 32);
 }
 
-// reduce hi*2^128 + lo with 2^128 = 0x2D00*2^32 - 1 (mod p)
-__device__ __forceinline__ felt reduce(const uint32_t r[8]) {
+// reduce hi*2^128 + lo with 2^128 = 0x2D00*2^32 - 1 (mod p): z (4 limbs) and k,
+// the carry past 2^128, with z + k*2^128 < 2^128 + 2^93 congruent to the input
+__device__ __forceinline__ void reduce_core(const uint32_t r[8], uint32_t& z0, uint32_t& z1, uint32_t& z2,
+                                            uint32_t& z3, uint64_t& k) {
   const uint32_t K = 0x2d00u;  // 45 * 2^8
   // q = H * K (5 limbs)
   uint64_t t = mul_wide(r[4], K);
@@ -273,13 +275,18 @@ __device__ __forceinline__ felt reduce(const uint32_t r[8]) {
   uint32_t y2 = addc_co(x2, u1, c, c);
   uint32_t y3 = addc_co_0(x3, c, c);
   uint64_t top = c;  // carry past 2^128
-  uint32_t z0 = sub_co(x0, x4, b);
-  uint32_t z1 = subb_co(y1, x5, b, b);
-  uint32_t z2 = subb_co_0(y2, b, b);
-  uint32_t z3 = subb_co_0(y3, b, b);
+  z0 = sub_co(x0, x4, b);
+  z1 = subb_co(y1, x5, b, b);
+  z2 = subb_co_0(y2, b, b);
+  z3 = subb_co_0(y3, b, b);
   // net bit 128 = top - borrow (>= 0 overall); set when top & !borrow
-  uint64_t k;
   ZKP_ASM("s_andn2_b64 %0, %1, %2" : "=s"(k) : "s"(top), "s"(b) : "scc");
+}
+
+__device__ __forceinline__ felt reduce(const uint32_t r[8]) {
+  uint32_t z0, z1, z2, z3;
+  uint64_t k;
+  reduce_core(r, z0, z1, z2, z3, k);
   return canon_rare(z0, z1, z2, z3, k);
 }
 
@@ -358,8 +365,9 @@ __device__ __forceinline__ void mul256x2(L4 x, L4 y, L4 u, L4 v, uint32_t r[8], 
   s[6] = (uint32_t)bcc; s[7] = (uint32_t)(bcc >> 32);
 }
 
-// Two independent reductions, interleaved like mul256x2.
-__device__ __forceinline__ void reduce_x2(const uint32_t r[8], const uint32_t s[8], felt& out_r, felt& out_s) {
+// Two independent reductions, interleaved like mul256x2 (z, k as reduce_core).
+__device__ __forceinline__ void reduce_x2_core(const uint32_t r[8], const uint32_t s[8], uint32_t z[4], uint32_t Z[4],
+                                               uint64_t& k1, uint64_t& k2) {
   const uint32_t K = 0x2d00u;
   uint64_t t = mul_wide(r[4], K), tt = mul_wide(s[4], K);
   uint32_t q0 = (uint32_t)t, p0 = (uint32_t)tt;
@@ -397,29 +405,34 @@ __device__ __forceinline__ void reduce_x2(const uint32_t r[8], const uint32_t s[
   uint32_t u1 = (uint32_t)(uu >> 32) + x5 * K, U1 = (uint32_t)(UU >> 32) + X5 * K;
   uint32_t y1 = add_co(x1, u0, c);
   uint32_t Y1 = add_co(X1, U0, e);
-  uint32_t z0 = sub_co(x0, x4, b);
-  uint32_t Z0 = sub_co(X0, X4, f);
+  z[0] = sub_co(x0, x4, b);
+  Z[0] = sub_co(X0, X4, f);
   uint32_t y2 = addc_co(x2, u1, c, c);
   uint32_t Y2 = addc_co(X2, U1, e, e);
-  uint32_t z1 = subb_co(y1, x5, b, b);
-  uint32_t Z1 = subb_co(Y1, X5, f, f);
+  z[1] = subb_co(y1, x5, b, b);
+  Z[1] = subb_co(Y1, X5, f, f);
   uint32_t y3 = addc_co_0(x3, c, c);
   uint32_t Y3 = addc_co_0(X3, e, e);
-  uint32_t z2 = subb_co_0(y2, b, b);
-  uint32_t Z2 = subb_co_0(Y2, f, f);
-  uint32_t z3 = subb_co_0(y3, b, b);
-  uint32_t Z3 = subb_co_0(Y3, f, f);
-  uint64_t k1, k2;
+  z[2] = subb_co_0(y2, b, b);
+  Z[2] = subb_co_0(Y2, f, f);
+  z[3] = subb_co_0(y3, b, b);
+  Z[3] = subb_co_0(Y3, f, f);
   ZKP_ASM("s_andn2_b64 %0, %1, %2" : "=s"(k1) : "s"(c), "s"(b) : "scc");
   ZKP_ASM("s_andn2_b64 %0, %1, %2" : "=s"(k2) : "s"(e), "s"(f) : "scc");
+}
+
+__device__ __forceinline__ void reduce_x2(const uint32_t r[8], const uint32_t s[8], felt& out_r, felt& out_s) {
+  uint32_t z[4], Z[4];
+  uint64_t k1, k2;
+  reduce_x2_core(r, s, z, Z, k1, k2);
   // canonical forms (canon_rare): one scalar branch for both products
-  const uint64_t rare = k1 | k2 | __builtin_amdgcn_ballot_w64(max(z3, Z3) == 0xffffffffu);
+  const uint64_t rare = k1 | k2 | __builtin_amdgcn_ballot_w64(max(z[3], Z[3]) == 0xffffffffu);
   if (rare) {
-    out_r = canon_from(z0, z1, z2, z3, k1);
-    out_s = canon_from(Z0, Z1, Z2, Z3, k2);
+    out_r = canon_from(z[0], z[1], z[2], z[3], k1);
+    out_s = canon_from(Z[0], Z[1], Z[2], Z[3], k2);
   } else {
-    out_r = join(z0, z1, z2, z3);
-    out_s = join(Z0, Z1, Z2, Z3);
+    out_r = join(z[0], z[1], z[2], z[3]);
+    out_s = join(Z[0], Z[1], Z[2], Z[3]);
   }
 }
 
@@ -429,4 +442,52 @@ __device__ __forceinline__ void mul_x2(felt a, felt b, felt c, felt d, felt& ab,
   reduce_x2(r, s, ab, cd);
 }
 
+// ---- deferred-check forms (the NTT rounds): no branch per operation. Each
+// result is taken as canonical and the evidence that it may not be — a carry
+// past 2^128 (k) or a top limb 0xffffffff — is accumulated in a Rare; a round
+// whose Rare is set is recomputed from its inputs with the exact forms. Valid
+// when every input is canonical, which holds until the first rare event.
+struct Rare {
+  uint64_t k = 0;    // OR of the products' carries past 2^128 (SGPR lane masks)
+  uint32_t top = 0;  // max of the results' top limbs
+  __device__ __forceinline__ bool any() const { return (k | __builtin_amdgcn_ballot_w64(top == 0xffffffffu)) != 0; }
+};
+
+__device__ __forceinline__ felt mul_z(felt a, felt b, Rare& q) {
+  uint32_t r[8], z0, z1, z2, z3;
+  uint64_t k;
+  mul256(split(a), split(b), r);
+  reduce_core(r, z0, z1, z2, z3, k);
+  q.k |= k;
+  q.top = max(q.top, z3);
+  return join(z0, z1, z2, z3);
+}
+
+__device__ __forceinline__ void mul_x2_z(felt a, felt b, felt c, felt d, felt& ab, felt& cd, Rare& q) {
+  uint32_t r[8], s[8], z[4], Z[4];
+  uint64_t k1, k2;
+  mul256x2(split(a), split(b), split(c), split(d), r, s);
+  reduce_x2_core(r, s, z, Z, k1, k2);
+  q.k |= k1 | k2;
+  q.top = max(q.top, max(z[3], Z[3]));
+  ab = join(z[0], z[1], z[2], z[3]);
+  cd = join(Z[0], Z[1], Z[2], Z[3]);
+}
+
+// a + b: carry set -> s + C (< p); carry clear -> s, canonical unless s3 = 0xffffffff
+__device__ __forceinline__ felt add_z(felt a, felt b, Rare& q) {
+  L4 x = split(a), y = split(b);
+  uint64_t c, g;
+  const uint32_t s0 = add_co(x.w0, y.w0, c);
+  const uint32_t s1 = addc_co(x.w1, y.w1, c, c);
+  const uint32_t s2 = addc_co(x.w2, y.w2, c, c);
+  const uint32_t s3 = addc_co(x.w3, y.w3, c, c);
+  q.top = max(q.top, s3);
+  const uint32_t m0 = sel_0_m1(c), m1 = m0 & C1;
+  const uint32_t t0 = add_co(s0, m0, g);
+  const uint32_t t1 = addc_co(s1, m1, g, g);
+  const uint32_t t2 = addc_co_0(s2, g, g);
+  const uint32_t t3 = addc_0(s3, g);
+  return join(t0, t1, t2, t3);
+}
 }  // namespace fpd

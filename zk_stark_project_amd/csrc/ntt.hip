@@ -111,24 +111,52 @@ __device__ __forceinline__ felt ntt_tw(const Ntt8Args& a, uint32_t j, uint32_t p
   return a.tw[((1u << lev) - 1) + j];
 }
 
-template <bool DIT>
-__device__ __forceinline__ void bfly(felt& x, felt& y, felt w) {
+// Butterflies of a register round. FAST: the deferred-check forms (fpd::mul_z,
+// add_z; the round's Rare decides whether it is recomputed with the exact forms,
+// FAST = false); the difference of canonical values needs no check.
+#if defined(__HIP_DEVICE_COMPILE__)
+using fpd::Rare;
+#else
+struct Rare {
+  bool any() const { return false; }
+};
+#endif
+
+template <bool FAST>
+__device__ __forceinline__ felt bmul(felt a, felt b, Rare& q) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  if constexpr (FAST) return fpd::mul_z(a, b, q);
+#endif
+  (void)q;
+  return mul(a, b);
+}
+template <bool FAST>
+__device__ __forceinline__ felt badd(felt a, felt b, Rare& q) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  if constexpr (FAST) return fpd::add_z(a, b, q);
+#endif
+  (void)q;
+  return add(a, b);
+}
+
+template <bool DIT, bool FAST>
+__device__ __forceinline__ void bfly(felt& x, felt& y, felt w, Rare& q) {
   if (DIT) {
-    felt t = mul(y, w);
+    felt t = bmul<FAST>(y, w, q);
     y = sub(x, t);
-    x = add(x, t);
+    x = badd<FAST>(x, t, q);
   } else {
     felt d = sub(x, y);
-    x = add(x, y);
-    y = mul(d, w);
+    x = badd<FAST>(x, y, q);
+    y = bmul<FAST>(d, w, q);
   }
 }
 
 // butterfly with twiddle 1 (no product)
-template <bool DIT>
-__device__ __forceinline__ void bfly1(felt& x, felt& y) {
+template <bool DIT, bool FAST>
+__device__ __forceinline__ void bfly1(felt& x, felt& y, Rare& q) {
   felt d = sub(x, y);
-  x = add(x, y);
+  x = badd<FAST>(x, y, q);
   y = d;
 }
 
@@ -151,22 +179,26 @@ struct NttRounds {
 
 // two independent butterflies with their products interleaved (fpd::mul_x2), so
 // each carry consumer sits two instructions after its producer
-template <bool DIT>
-__device__ __forceinline__ void bfly2(felt& x0, felt& y0, felt w0, felt& x1, felt& y1, felt w1) {
+template <bool DIT, bool FAST>
+__device__ __forceinline__ void bfly2(felt& x0, felt& y0, felt w0, felt& x1, felt& y1, felt w1, Rare& q) {
 #if defined(__HIP_DEVICE_COMPILE__)
+  auto mx2 = [&](felt a, felt b, felt c, felt d, felt& ab, felt& cd) {
+    if constexpr (FAST) fpd::mul_x2_z(a, b, c, d, ab, cd, q);
+    else fpd::mul_x2(a, b, c, d, ab, cd);
+  };
   if (DIT) {
     felt t0, t1;
-    fpd::mul_x2(y0, w0, y1, w1, t0, t1);
-    y0 = sub(x0, t0); x0 = add(x0, t0);
-    y1 = sub(x1, t1); x1 = add(x1, t1);
+    mx2(y0, w0, y1, w1, t0, t1);
+    y0 = sub(x0, t0); x0 = badd<FAST>(x0, t0, q);
+    y1 = sub(x1, t1); x1 = badd<FAST>(x1, t1, q);
   } else {
     felt d0 = sub(x0, y0), d1 = sub(x1, y1);
-    x0 = add(x0, y0); x1 = add(x1, y1);
-    fpd::mul_x2(d0, w0, d1, w1, y0, y1);
+    x0 = badd<FAST>(x0, y0, q); x1 = badd<FAST>(x1, y1, q);
+    mx2(d0, w0, d1, w1, y0, y1);
   }
 #else
-  bfly<DIT>(x0, y0, w0);
-  bfly<DIT>(x1, y1, w1);
+  bfly<DIT, FAST>(x0, y0, w0, q);
+  bfly<DIT, FAST>(x1, y1, w1, q);
 #endif
 }
 
@@ -239,14 +271,21 @@ __global__ __launch_bounds__(NT) void k_ntt8(Ntt8Args a) {
     return ((hi0 + hl) << (lo + K)) + (q << lo) + l0 + ll;
   };
   if (staged) {
+    // coset scale with the deferred check (the loads are redone exactly if it trips)
+    auto stage_in = [&](auto fast_c, Rare& q) {
+      constexpr bool FAST = decltype(fast_c)::value;
 #pragma unroll
-    for (int i = 0; i < 8; i++) {
-      uint32_t slot;
-      uint32_t ad = staged_elem(tid + i * NT, slot);
-      felt v = src[ad];
-      if (scale) v = mul(v, scale[ad]);
-      lds[slot] = v;
-    }
+      for (int i = 0; i < 8; i++) {
+        uint32_t slot;
+        uint32_t ad = staged_elem(tid + i * NT, slot);
+        felt v = src[ad];
+        if (scale) v = bmul<FAST>(v, scale[ad], q);
+        lds[slot] = v;
+      }
+    };
+    Rare q;
+    stage_in(std::true_type{}, q);
+    if (scale && q.any()) stage_in(std::false_type{}, q);
     __syncthreads();
   }
   uint32_t b0 = DIT ? 0 : K;
@@ -258,25 +297,36 @@ __global__ __launch_bounds__(NT) void k_ntt8(Ntt8Args a) {
     if (!first) __syncthreads();
     felt x[8];
     uint32_t ggs[2], qlow[2];
-    // block-local coordinates (gg, q) of register m in this round
-    auto coord_gg = [&](int m) { return ((uint32_t)(m >> rb) << LOGNT | tid) & (T - 1); };
-    auto coord_q = [&](int m) {
+    // block-local coordinates (gg, q) of register m in this round (for thread tr)
+    auto coord_gg = [&](int m, uint32_t tr) { return ((uint32_t)(m >> rb) << LOGNT | tr) & (T - 1); };
+    auto coord_q = [&](int m, uint32_t tr) {
       uint32_t extra = m >> rb, bf = m & ((1u << rb) - 1);
-      uint32_t qo = ((extra << LOGNT) | tid) >> logT;
+      uint32_t qo = ((extra << LOGNT) | tr) >> logT;
       uint32_t ql = qo & ((1u << b0) - 1);
       return ((qo >> b0) << (b0 + rb)) | (bf << b0) | ql;
     };
+    // the round: its inputs (HBM + coset scale, or LDS, which stays intact until
+    // the barrier below), then its butterflies. It runs with the deferred-check
+    // forms, and again with the exact ones when a lane of the wave saw a carry past
+    // 2^128 or a top limb 0xffffffff: one scalar branch per round.
+    // The exact pass derives every index from an opaque copy of the thread id, so
+    // nothing it loads is shared with (and kept live across) the fast pass.
+    auto round = [&](auto fast_c, Rare& qq) {
+    constexpr bool FAST = decltype(fast_c)::value;
+    uint32_t tr = tid;
+    if constexpr (!FAST) asm volatile("" : "+v"(tr));
+    const uint32_t zo = tr - tid;  // 0, opaque on the exact pass
 #pragma unroll
     for (int m = 0; m < 8; m++) {
       uint32_t extra = m >> rb, bf = m & ((1u << rb) - 1);
-      uint32_t c = (extra << LOGNT) | tid;
+      uint32_t c = (extra << LOGNT) | tr;
       if (first && !staged) {  // straight from HBM (coalesced along gg), coset scale fused
-        uint32_t ad = gaddr(coord_gg(m), coord_q(m));
+        uint32_t ad = gaddr(coord_gg(m, tr), coord_q(m, tr));
         felt v = src[ad];
-        if (scale) v = mul(v, scale[ad]);
+        if (scale) v = bmul<FAST>(v, scale[ad], qq);
         x[m] = v;
       } else {
-        x[m] = lds[lidx(coord_q(m), coord_gg(m))];
+        x[m] = lds[lidx(coord_q(m, tr), coord_gg(m, tr))];
       }
       if (bf == 0 && extra < 2) { ggs[extra] = c & (T - 1); qlow[extra] = (c >> logT) & ((1u << b0) - 1); }
     }
@@ -287,63 +337,63 @@ __global__ __launch_bounds__(NT) void k_ntt8(Ntt8Args a) {
       // stages 0..2 (b0 = 0, lo = 0, so jb = 0): 7 of the 12 products are by 1
       constexpr bool smallest = SMALL && (DIT ? first : last);
       if constexpr (DIT && smallest) {
-        bfly1<true>(x[0], x[1]); bfly1<true>(x[2], x[3]); bfly1<true>(x[4], x[5]); bfly1<true>(x[6], x[7]);
-        const felt w1 = ntt_tw<true>(a, 1, 1);
-        bfly1<true>(x[0], x[2]); bfly1<true>(x[4], x[6]);
-        bfly2<true>(x[1], x[3], w1, x[5], x[7], w1);
-        const felt w21 = ntt_tw<true>(a, 1, 2), w22 = ntt_tw<true>(a, 2, 2), w23 = ntt_tw<true>(a, 3, 2);
-        bfly1<true>(x[0], x[4]);
-        bfly2<true>(x[1], x[5], w21, x[2], x[6], w22);
-        bfly<true>(x[3], x[7], w23);
+        bfly1<true, FAST>(x[0], x[1], qq); bfly1<true, FAST>(x[2], x[3], qq); bfly1<true, FAST>(x[4], x[5], qq); bfly1<true, FAST>(x[6], x[7], qq);
+        const felt w1 = ntt_tw<true>(a, 1 + zo, 1);
+        bfly1<true, FAST>(x[0], x[2], qq); bfly1<true, FAST>(x[4], x[6], qq);
+        bfly2<true, FAST>(x[1], x[3], w1, x[5], x[7], w1, qq);
+        const felt w21 = ntt_tw<true>(a, 1 + zo, 2), w22 = ntt_tw<true>(a, 2 + zo, 2), w23 = ntt_tw<true>(a, 3 + zo, 2);
+        bfly1<true, FAST>(x[0], x[4], qq);
+        bfly2<true, FAST>(x[1], x[5], w21, x[2], x[6], w22, qq);
+        bfly<true, FAST>(x[3], x[7], w23, qq);
       } else if constexpr (!DIT && smallest) {
-        const felt w21 = ntt_tw<false>(a, 1, 2), w22 = ntt_tw<false>(a, 2, 2), w23 = ntt_tw<false>(a, 3, 2);
-        bfly1<false>(x[0], x[4]);
-        bfly2<false>(x[1], x[5], w21, x[2], x[6], w22);
-        bfly<false>(x[3], x[7], w23);
-        const felt w1 = ntt_tw<false>(a, 1, 1);
-        bfly1<false>(x[0], x[2]); bfly1<false>(x[4], x[6]);
-        bfly2<false>(x[1], x[3], w1, x[5], x[7], w1);
-        bfly1<false>(x[0], x[1]); bfly1<false>(x[2], x[3]); bfly1<false>(x[4], x[5]); bfly1<false>(x[6], x[7]);
+        const felt w21 = ntt_tw<false>(a, 1 + zo, 2), w22 = ntt_tw<false>(a, 2 + zo, 2), w23 = ntt_tw<false>(a, 3 + zo, 2);
+        bfly1<false, FAST>(x[0], x[4], qq);
+        bfly2<false, FAST>(x[1], x[5], w21, x[2], x[6], w22, qq);
+        bfly<false, FAST>(x[3], x[7], w23, qq);
+        const felt w1 = ntt_tw<false>(a, 1 + zo, 1);
+        bfly1<false, FAST>(x[0], x[2], qq); bfly1<false, FAST>(x[4], x[6], qq);
+        bfly2<false, FAST>(x[1], x[3], w1, x[5], x[7], w1, qq);
+        bfly1<false, FAST>(x[0], x[1], qq); bfly1<false, FAST>(x[2], x[3], qq); bfly1<false, FAST>(x[4], x[5], qq); bfly1<false, FAST>(x[6], x[7], qq);
       } else if constexpr (DIT) {
         {
           felt w0 = ntt_tw<true>(a, jb, b0);
-          bfly2<true>(x[0], x[1], w0, x[2], x[3], w0); bfly2<true>(x[4], x[5], w0, x[6], x[7], w0);
+          bfly2<true, FAST>(x[0], x[1], w0, x[2], x[3], w0, qq); bfly2<true, FAST>(x[4], x[5], w0, x[6], x[7], w0, qq);
         }
         {
           felt w1a = ntt_tw<true>(a, jb, b0 + 1);
           felt w1b = ntt_tw<true>(a, jb | jstep, b0 + 1);
-          bfly2<true>(x[0], x[2], w1a, x[1], x[3], w1b); bfly2<true>(x[4], x[6], w1a, x[5], x[7], w1b);
+          bfly2<true, FAST>(x[0], x[2], w1a, x[1], x[3], w1b, qq); bfly2<true, FAST>(x[4], x[6], w1a, x[5], x[7], w1b, qq);
         }
         static_for<0, 2>([&](auto k2) {
           felt w2a = ntt_tw<true>(a, jb | ((uint32_t)(2 * k2) << (b0 + lo)), b0 + 2);
           felt w2b = ntt_tw<true>(a, jb | ((uint32_t)(2 * k2 + 1) << (b0 + lo)), b0 + 2);
-          bfly2<true>(x[2 * k2], x[2 * k2 + 4], w2a, x[2 * k2 + 1], x[2 * k2 + 5], w2b);
+          bfly2<true, FAST>(x[2 * k2], x[2 * k2 + 4], w2a, x[2 * k2 + 1], x[2 * k2 + 5], w2b, qq);
         });
       } else {
         static_for<0, 2>([&](auto k2) {
           felt w2a = ntt_tw<false>(a, jb | ((uint32_t)(2 * k2) << (b0 + lo)), b0 + 2);
           felt w2b = ntt_tw<false>(a, jb | ((uint32_t)(2 * k2 + 1) << (b0 + lo)), b0 + 2);
-          bfly2<false>(x[2 * k2], x[2 * k2 + 4], w2a, x[2 * k2 + 1], x[2 * k2 + 5], w2b);
+          bfly2<false, FAST>(x[2 * k2], x[2 * k2 + 4], w2a, x[2 * k2 + 1], x[2 * k2 + 5], w2b, qq);
         });
         {
           felt w1a = ntt_tw<false>(a, jb, b0 + 1);
           felt w1b = ntt_tw<false>(a, jb | jstep, b0 + 1);
-          bfly2<false>(x[0], x[2], w1a, x[1], x[3], w1b); bfly2<false>(x[4], x[6], w1a, x[5], x[7], w1b);
+          bfly2<false, FAST>(x[0], x[2], w1a, x[1], x[3], w1b, qq); bfly2<false, FAST>(x[4], x[6], w1a, x[5], x[7], w1b, qq);
         }
         {
           felt w0 = ntt_tw<false>(a, jb, b0);
-          bfly2<false>(x[0], x[1], w0, x[2], x[3], w0); bfly2<false>(x[4], x[5], w0, x[6], x[7], w0);
+          bfly2<false, FAST>(x[0], x[1], w0, x[2], x[3], w0, qq); bfly2<false, FAST>(x[4], x[5], w0, x[6], x[7], w0, qq);
         }
       }
     } else if constexpr (rb == 2) {
       if constexpr (!DIT && SMALL && last) {  // DIF stages 1, 0: one product of four is not by 1
-        const felt w1 = ntt_tw<false>(a, 1, 1);
+        const felt w1 = ntt_tw<false>(a, 1 + zo, 1);
 #pragma unroll
         for (int u = 0; u < 2; u++) {
           felt* y = x + 4 * u;
-          bfly1<false>(y[0], y[2]);
-          bfly<false>(y[1], y[3], w1);
-          bfly1<false>(y[0], y[1]); bfly1<false>(y[2], y[3]);
+          bfly1<false, FAST>(y[0], y[2], qq);
+          bfly<false, FAST>(y[1], y[3], w1, qq);
+          bfly1<false, FAST>(y[0], y[1], qq); bfly1<false, FAST>(y[2], y[3], qq);
         }
       } else {
 #pragma unroll
@@ -354,29 +404,33 @@ __global__ __launch_bounds__(NT) void k_ntt8(Ntt8Args a) {
         felt w1a = ntt_tw<DIT>(a, jb, b0 + 1), w1b = ntt_tw<DIT>(a, jb | (1u << (b0 + lo)), b0 + 1);
         felt* y = x + 4 * u;
         if (DIT) {
-          bfly2<true>(y[0], y[1], w0, y[2], y[3], w0);
-          bfly2<true>(y[0], y[2], w1a, y[1], y[3], w1b);
+          bfly2<true, FAST>(y[0], y[1], w0, y[2], y[3], w0, qq);
+          bfly2<true, FAST>(y[0], y[2], w1a, y[1], y[3], w1b, qq);
         } else {
-          bfly2<false>(y[0], y[2], w1a, y[1], y[3], w1b);
-          bfly2<false>(y[0], y[1], w0, y[2], y[3], w0);
+          bfly2<false, FAST>(y[0], y[2], w1a, y[1], y[3], w1b, qq);
+          bfly2<false, FAST>(y[0], y[1], w0, y[2], y[3], w0, qq);
         }
       }
       }
     } else {
 #pragma unroll
       for (int u = 0; u < 4; u++) {
-        uint32_t c = ((uint32_t)u << LOGNT) | tid;
+        uint32_t c = ((uint32_t)u << LOGNT) | tr;
         uint32_t gg = c & (T - 1);
         uint32_t ql = (c >> logT) & ((1u << b0) - 1);
         const uint32_t jb = (ql << lo) | (l0 + (gg & (Tl - 1)));
-        bfly<DIT>(x[2 * u], x[2 * u + 1], ntt_tw<DIT>(a, jb, b0));
+        bfly<DIT, FAST>(x[2 * u], x[2 * u + 1], ntt_tw<DIT>(a, jb, b0), qq);
       }
     }
+    };
+    Rare qq;
+    round(std::true_type{}, qq);
+    if (qq.any()) round(std::false_type{}, qq);
     if (!last || staged) __syncthreads();  // everyone has read this round's slots
 #pragma unroll
     for (int m = 0; m < 8; m++) {
-      if (last && !staged) dst[gaddr(coord_gg(m), coord_q(m))] = x[m];  // straight to HBM
-      else lds[lidx(coord_q(m), coord_gg(m))] = x[m];
+      if (last && !staged) dst[gaddr(coord_gg(m, tid), coord_q(m, tid))] = x[m];  // straight to HBM
+      else lds[lidx(coord_q(m, tid), coord_gg(m, tid))] = x[m];
     }
     if (DIT) b0 += rb;
   });
