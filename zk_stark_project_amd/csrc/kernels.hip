@@ -335,17 +335,28 @@ __global__ __launch_bounds__(TPB) void k_eval_mimc(EvalCommon c, MimcEvalArgs a,
     const uint64_t q = EVAL_POINT(k);
     if (q >= M) return;
     const CePoint pt = ce_point(c, q);
-    felt cur = lde[pt.off];
-    felt nxt = lde[pt.off_next];
-    felt kv = a.kper[pt.s & kmask];
-    felt x = point_x(c.pm, q);
-    felt u = add(cur, kv);
-    felt u2 = sqr(u), u3 = mul(u2, u), u6 = sqr(u3), u7 = mul(u6, u);
-    felt tr = sub(nxt, u7);  // coef_t is folded into c.zinv (per CE coset)
-    felt e0 = sub(x, one()), e1 = sub(x, c.w_last);
-    felt tpart = mul(mul(tr, e1), c.zinv[pt.u]);
-    felt bnum = add(mul(mul(b0, sub(cur, a.v0)), e1), mul(mul(b1, sub(cur, a.v1)), e0));
-    comp[q] = add(tpart, mul(bnum, dinv[q]));  // dinv = 1/((x - 1)(x - w^(n-1)))
+    const felt cur = lde[pt.off];
+    const felt nxt = lde[pt.off_next];
+    const felt kv = a.kper[pt.s & kmask];
+    const felt zi = c.zinv[pt.u], di = dinv[q];
+    // the point with the deferred-check forms, again with the exact ones if a lane
+    // of the wave needs it (kernels_common.hpp dmul / dadd)
+    auto point = [&](auto fast_c, Rare& rq) {
+      constexpr bool F = decltype(fast_c)::value;
+      felt x = dmul<F>(c.pm.cx[q >> c.pm.logn], tw_full(c.pm.twn, q & ((1ull << c.pm.logn) - 1), c.pm.logn), rq);
+      felt u = dadd<F>(cur, kv, rq);
+      felt u2 = dmul<F>(u, u, rq), u3 = dmul<F>(u2, u, rq), u6 = dmul<F>(u3, u3, rq), u7 = dmul<F>(u6, u, rq);
+      felt tr = sub(nxt, u7);  // coef_t is folded into c.zinv (per CE coset)
+      felt e0 = sub(x, one()), e1 = sub(x, c.w_last);
+      felt tpart = dmul<F>(dmul<F>(tr, e1, rq), zi, rq);
+      felt bnum = dadd<F>(dmul<F>(dmul<F>(b0, sub(cur, a.v0), rq), e1, rq),
+                          dmul<F>(dmul<F>(b1, sub(cur, a.v1), rq), e0, rq), rq);
+      return dadd<F>(tpart, dmul<F>(bnum, di, rq), rq);  // dinv = 1/((x - 1)(x - w^(n-1)))
+    };
+    Rare rq;
+    felt v = point(std::true_type{}, rq);
+    if (rq.any()) v = point(std::false_type{}, rq);
+    comp[q] = v;
   });
 }
 

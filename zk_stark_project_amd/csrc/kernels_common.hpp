@@ -19,7 +19,45 @@ using namespace fp;
     (prof).end(stream);                                         \
   } while (0)
 
+// Deferred-check field ops (felt_dev.hpp fpd::Rare). dmul / dadd with FAST take
+// every result as canonical and record the evidence that one may not be (a carry
+// past 2^128, a top limb 0xffffffff); a kernel whose Rare is set recomputes its
+// values with FAST = false, the exact forms. kc::opaque_tid gives that exact pass
+// thread indices the compiler cannot match with the fast pass's, so nothing the
+// fast pass loaded is kept live for it.
+#if defined(__HIP_DEVICE_COMPILE__)
+using Rare = fpd::Rare;
+#else
+struct Rare {
+  bool any() const { return false; }
+};
+#endif
+
+template <bool FAST>
+__device__ __forceinline__ felt dmul(felt a, felt b, Rare& q) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  if constexpr (FAST) return fpd::mul_z(a, b, q);
+#endif
+  (void)q;
+  return mul(a, b);
+}
+template <bool FAST>
+__device__ __forceinline__ felt dadd(felt a, felt b, Rare& q) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  if constexpr (FAST) return fpd::add_z(a, b, q);
+#endif
+  (void)q;
+  return add(a, b);
+}
+
 namespace kc {
+
+template <bool FAST>
+__device__ __forceinline__ uint32_t opaque_tid() {
+  uint32_t t = threadIdx.x;
+  if constexpr (!FAST) asm volatile("" : "+v"(t));
+  return t;
+}
 
 __device__ __forceinline__ uint32_t rev_bits(uint32_t x, uint32_t bits) {
   return bits == 0 ? 0u : (__brev(x) >> (32 - bits));

@@ -111,33 +111,13 @@ __device__ __forceinline__ felt ntt_tw(const Ntt8Args& a, uint32_t j, uint32_t p
   return a.tw[((1u << lev) - 1) + j];
 }
 
-// Butterflies of a register round. FAST: the deferred-check forms (fpd::mul_z,
-// add_z; the round's Rare decides whether it is recomputed with the exact forms,
+// Butterflies of a register round. FAST: the deferred-check forms (dmul, dadd;
+// the round's Rare decides whether it is recomputed with the exact forms,
 // FAST = false); the difference of canonical values needs no check.
-#if defined(__HIP_DEVICE_COMPILE__)
-using fpd::Rare;
-#else
-struct Rare {
-  bool any() const { return false; }
-};
-#endif
-
 template <bool FAST>
-__device__ __forceinline__ felt bmul(felt a, felt b, Rare& q) {
-#if defined(__HIP_DEVICE_COMPILE__)
-  if constexpr (FAST) return fpd::mul_z(a, b, q);
-#endif
-  (void)q;
-  return mul(a, b);
-}
+__device__ __forceinline__ felt bmul(felt a, felt b, Rare& q) { return dmul<FAST>(a, b, q); }
 template <bool FAST>
-__device__ __forceinline__ felt badd(felt a, felt b, Rare& q) {
-#if defined(__HIP_DEVICE_COMPILE__)
-  if constexpr (FAST) return fpd::add_z(a, b, q);
-#endif
-  (void)q;
-  return add(a, b);
-}
+__device__ __forceinline__ felt badd(felt a, felt b, Rare& q) { return dadd<FAST>(a, b, q); }
 
 template <bool DIT, bool FAST>
 __device__ __forceinline__ void bfly(felt& x, felt& y, felt w, Rare& q) {
