@@ -63,7 +63,7 @@ KERNEL_STAGES = {
     "eval_mimc": ("eval",), "eval_linear": ("eval",),
 }
 UBENCH_BFLY = "profiles/r04_ubench_bfly.json"  # tests/native/ubench_bfly.hip on the box: the butterfly floor
-PMC_TAGS = ("r03", "r02_final", "r02", "r01")  # newest committed PMC summaries first (scripts/profile_round.sh)
+PMC_TAGS = ("r04", "r03", "r02_final", "r02", "r01")  # newest committed PMC summaries first (scripts/profile_round.sh)
 
 
 def stage_bytes(w: int, n: int, B: int, ce: int, C: int, rem: int = 7, F: int = 16) -> dict:
@@ -192,9 +192,12 @@ def valu_side(kernel: str, air: str, mode: str):
 
 def isa_mix() -> dict:
     """kernel symbol (as the rocprofv3 summaries name it) -> share of 4-cycle VALU
-    instructions in its gfx950 ISA (profiles/r02_isa_mix.json, scripts/isa_mix.py)."""
-    path = os.path.join(ROOT, "profiles", "r02_isa_mix.json")
-    if not os.path.exists(path):
+    instructions in its gfx950 ISA (profiles/r0*_isa_mix.json, scripts/isa_mix.py)."""
+    for name in ("r04_isa_mix.json", "r02_isa_mix.json"):  # newest first
+        path = os.path.join(ROOT, "profiles", name)
+        if os.path.exists(path):
+            break
+    else:
         return {}
     with open(path) as f:
         d = json.load(f)

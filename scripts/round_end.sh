@@ -3,7 +3,7 @@
 # check), the C2 timeline, then rocprofv3 kernel-trace + PMC passes for C2 and C3.
 #   scripts/round_end.sh <tag>   -> gpurun_out/b_c2.json, b_c3.json, timeline_<tag>.txt, prof_<tag>{,agg}/
 set -o pipefail
-TAG=${1:-r03}
+TAG=${1:-r04}
 mkdir -p gpurun_out
 timeout -k 10 300 python bench.py --steps 20 --stats > gpurun_out/b_c2.json 2> gpurun_out/b_c2.err || { tail -20 gpurun_out/b_c2.err; exit 1; }
 timeout -k 10 240 python bench.py --air agg --steps 10 --no-cpu-baseline --stats > gpurun_out/b_c3.json 2> gpurun_out/b_c3.err || { tail -20 gpurun_out/b_c3.err; exit 1; }
