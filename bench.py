@@ -395,15 +395,18 @@ def session_leg(ctx, wl, pub, tr, steps: int) -> dict:
     def once():
         return _native.prove_by_stages(ctx, wl["air_id"], wl["trace"].data, pub, wl["opts"], NUM_COEFFS[air])
     got = once()  # warm (the session context's domain tables)
+    stage_ms = {}
     t0 = time.perf_counter()
     for _ in range(steps):
-        got = once()
+        got = _native.prove_by_stages(ctx, wl["air_id"], wl["trace"].data, pub, wl["opts"], NUM_COEFFS[air],
+                                      times=stage_ms)
     ms = (time.perf_counter() - t0) / steps * 1e3
     want = tr.summary()
     same = (got["trace_root"].hex() == want["trace_root"] and got["constraint_root"].hex() == want["constraint_root"]
             and [r.hex() for r in got["fri_roots"]] == want["fri_roots"] and got["z"] == want["z"]
             and got["pow_nonce"] == want["pow_nonce"] and got["query_positions"] == want["query_positions"])
     return {"session_ms": round(ms, 3), "steps": steps, "equals_zkp_prove_transcript": same,
+            "stage_ms": {k: round(v / steps, 3) for k, v in stage_ms.items()},
             "route": "zkp_session_trace_lde -> zkp_eval_constraints -> zkp_composition_commit -> zkp_ood_frame -> "
                      "zkp_deep_fri -> zkp_grind -> zkp_query, coefficients from zkp_channel (host)"}
 

@@ -1,0 +1,17 @@
+#!/bin/bash
+# Round-4 GPU check, second form: the non-slow GPU suite, a C2 bench line and a C3
+# bench line (both with the session leg and its per-stage times).
+set -o pipefail
+mkdir -p gpurun_out
+timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests -m "gpu and not slow" \
+  > gpurun_out/check_tests.log 2>&1 || { tail -40 gpurun_out/check_tests.log; exit 1; }
+tail -2 gpurun_out/check_tests.log
+timeout -k 10 400 python bench.py --steps 20 --no-cpu-baseline > gpurun_out/b_c2.json 2> gpurun_out/b_c2.err || { tail -20 gpurun_out/b_c2.err; exit 1; }
+timeout -k 10 400 python bench.py --air agg --steps 10 --no-cpu-baseline > gpurun_out/b_c3.json 2> gpurun_out/b_c3.err || { tail -20 gpurun_out/b_c3.err; exit 1; }
+python3 -c "
+import json
+for f in ('b_c2', 'b_c3'):
+    d=json.loads(open('gpurun_out/%s.json' % f).read().strip().splitlines()[-1])
+    print(f, d['value'], d['ms_per_step'], d['device_resident_ms'], d['roofline']['frac'], d['roofline']['valu_floor_frac'])
+    print('  session', d['session']['session_ms'], d['session']['equals_zkp_prove_transcript'], d['session'].get('stage_ms'))
+"

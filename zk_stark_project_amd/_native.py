@@ -9,6 +9,7 @@ from __future__ import annotations
 import ctypes
 import os
 import threading
+import time
 
 import numpy as np
 
@@ -643,22 +644,35 @@ class Channel:
 
 
 def prove_by_stages(ctx: "Context", air_id: int, trace: np.ndarray, pub, options: ProofOptions,
-                    num_coeffs: int) -> dict:
+                    num_coeffs: int, times: dict | None = None) -> dict:
     """One proof through the stage hooks, in generate_proof's order, with the host
     channel drawing every coefficient (what a winter-prover fork's `Prover::prove`
     does with its own channel). Returns the commitments, z, nonce, positions and the
-    query section; they equal zkp_prove's for the same trace."""
+    query section; they equal zkp_prove's for the same trace. `times` (optional)
+    accumulates the wall-clock ms of each stage call under its entry point's name."""
     w, n = int(trace.shape[0]), int(trace.shape[1])
+    clock = [time.perf_counter()]
+
+    def lap(name):
+        if times is not None:
+            t = time.perf_counter()
+            times[name] = times.get(name, 0.0) + (t - clock[0]) * 1e3
+            clock[0] = t
     ch = Channel(air_id, w, n, pub, options)
     s = Session(ctx, air_id, w, n, pub, options)
+    lap("create")
     try:
         troot = s.trace_lde(trace)
+        lap("trace_lde")
         ch.commit(troot)
         s.eval_constraints(ch.draw_coeffs(options.batching_constraints, num_coeffs), want_evals=False)
+        lap("eval_constraints")
         croot = s.composition_commit()
+        lap("composition_commit")
         ch.commit(croot)
         z = ch.draw()
         tood, cood = s.ood_frame(z)
+        lap("ood_frame")
         ch.commit_felts(tood)
         ch.commit_felts(cood)
         gam = ch.draw_coeffs(options.batching_deep, w + s.num_columns)
@@ -669,10 +683,13 @@ def prove_by_stages(ctx: "Context", air_id: int, trace: np.ndarray, pub, options
             ch.commit(root)
             return ch.draw()
         rem, rcommit = s.deep_fri(gam, fri_channel)
+        lap("deep_fri")
         ch.commit(rcommit)
         nonce = ctx.grind(ch.seed(), options.grinding_factor) if options.grinding_factor else 1
+        lap("grind")
         pos = ch.query_positions(nonce)
         queries = s.query(pos)
+        lap("query")
     finally:
         s.close()
         ch.close()

@@ -107,7 +107,7 @@ __global__ __launch_bounds__(TPB) void k_comp_dft(const felt* __restrict__ recv,
 //  MIMC  : out[u] = zinv[u] * cc[0] (u < ce), out[ce] = cc[1], out[ce+1] = cc[2]
 //  GLOBAL_UPDATE (w = 120): out[0..4w) = lin coefs, out[4w] = sum_c cc[num_t+c]*aval[c], out[4w+1] = 0
 //  TRAINING_UPDATE (half = w/2): out[0..4half) = lin coefs, out[4half] / [4half+1] = the two boundary sums
-__global__ __launch_bounds__(TPB) void k_dt_eval_consts(int air, const felt* __restrict__ cc, felt k,
+__global__ __launch_bounds__(TPB) void k_dt_eval_consts(int air, const felt* __restrict__ cc, felt k, felt wl,
                                                         const felt* __restrict__ aval, const felt* __restrict__ zinv,
                                                         uint32_t ce, uint32_t w, uint32_t num_t,
                                                         felt* __restrict__ out) {
@@ -115,7 +115,16 @@ __global__ __launch_bounds__(TPB) void k_dt_eval_consts(int air, const felt* __r
   const uint32_t t = threadIdx.x;
   if (air == ZKP_AIR_MIMC) {
     for (uint32_t u = t; u < ce; u += TPB) out[u] = mul(zinv[u], cc[0]);
-    if (t == 0) { out[ce] = cc[1]; out[ce + 1] = cc[2]; }
+    // the boundary numerator b0 (cur - v0)(x - wl) + b1 (cur - v1)(x - 1)
+    //   = cur (x A - Bc) - x Cc + D,  A = b0 + b1, Bc = b0 wl + b1,
+    //   Cc = b0 v0 + b1 v1, D = b0 v0 wl + b1 v1  (three products per point, not four)
+    if (t == 0) {
+      const felt b0 = cc[1], b1 = cc[2], c0 = mul(b0, aval[0]), c1 = mul(b1, aval[1]);
+      out[ce] = add(b0, b1);
+      out[ce + 1] = add(mul(b0, wl), b1);
+      out[ce + 2] = add(c0, c1);
+      out[ce + 3] = add(mul(c0, wl), c1);
+    }
     return;
   }
   const bool gu = air == ZKP_AIR_GLOBAL_UPDATE;
@@ -330,7 +339,7 @@ __global__ __launch_bounds__(TPB) void k_eval_mimc(EvalCommon c, MimcEvalArgs a,
                                                    const felt* __restrict__ dinv, felt* __restrict__ comp) {
   const uint64_t M = (uint64_t)c.cel << c.logn;
   const uint64_t kmask = (64ull << c.logce) - 1;
-  const felt b0 = a.bcoef[0], b1 = a.bcoef[1];
+  const felt bA = a.bcoef[0], bB = a.bcoef[1], bC = a.bcoef[2], bD = a.bcoef[3];
   static_for<0, EVAL_CH>([&](auto k) {
     const uint64_t q = EVAL_POINT(k);
     if (q >= M) return;
@@ -347,10 +356,9 @@ __global__ __launch_bounds__(TPB) void k_eval_mimc(EvalCommon c, MimcEvalArgs a,
       felt u = dadd<F>(cur, kv, rq);
       felt u2 = dmul<F>(u, u, rq), u3 = dmul<F>(u2, u, rq), u6 = dmul<F>(u3, u3, rq), u7 = dmul<F>(u6, u, rq);
       felt tr = sub(nxt, u7);  // coef_t is folded into c.zinv (per CE coset)
-      felt e0 = sub(x, one()), e1 = sub(x, c.w_last);
-      felt tpart = dmul<F>(dmul<F>(tr, e1, rq), zi, rq);
-      felt bnum = dadd<F>(dmul<F>(dmul<F>(b0, sub(cur, a.v0), rq), e1, rq),
-                          dmul<F>(dmul<F>(b1, sub(cur, a.v1), rq), e0, rq), rq);
+      felt tpart = dmul<F>(dmul<F>(tr, sub(x, c.w_last), rq), zi, rq);
+      // b0 (cur - v0)(x - w_last) + b1 (cur - v1)(x - 1), regrouped (k_dt_eval_consts)
+      felt bnum = add(sub(dmul<F>(cur, sub(dmul<F>(x, bA, rq), bB), rq), dmul<F>(x, bC, rq)), bD);
       return dadd<F>(tpart, dmul<F>(bnum, di, rq), rq);  // dinv = 1/((x - 1)(x - w^(n-1)))
     };
     Rare rq;
@@ -1210,10 +1218,10 @@ void launch_gu_trace(Prof& prof, hipStream_t s, const felt* masked, const felt* 
                             kinv, n, tile_buf, out));
 }
 
-void launch_dt_eval_consts(Prof& prof, hipStream_t s, int air, const felt* cc, felt k, const felt* aval,
+void launch_dt_eval_consts(Prof& prof, hipStream_t s, int air, const felt* cc, felt k, felt w_last, const felt* aval,
                            const felt* zinv, uint32_t ce, uint32_t w, uint32_t num_t, felt* out) {
   LAUNCH(prof, "coin", s, 0.0,
-         hipLaunchKernelGGL(k_dt_eval_consts, dim3(1), dim3(TPB), 0, s, air, cc, k, aval, zinv, ce, w, num_t, out));
+         hipLaunchKernelGGL(k_dt_eval_consts, dim3(1), dim3(TPB), 0, s, air, cc, k, w_last, aval, zinv, ce, w, num_t, out));
 }
 
 void launch_gu_check(Prof& prof, hipStream_t s, const felt* T, uint32_t d, uint32_t logn, felt k, uint32_t c0,

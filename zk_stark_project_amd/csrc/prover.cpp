@@ -539,8 +539,8 @@ void constraint_eval(zkp_ctx* ctx, const AirDesc& air, uint32_t logn, uint32_t l
   // (MiMC: Z_T constants with the transition coefficient folded in, then b0, b1;
   // linear AIRs: the 4 coefficient rows + the two boundary sums)
   const uint32_t lw = air.id == ZKP_AIR_TRAINING_UPDATE ? w / 2 : w;
-  felt* dconst = ctx->buf<felt>("eval_consts", air.id == ZKP_AIR_MIMC ? (size_t)ce + 2 : 4 * (size_t)lw + 2);
-  launch_dt_eval_consts(pf, st, air.id, dt_cc, air.k, dt_aval, dz, ce, w, air.num_t, dconst);
+  felt* dconst = ctx->buf<felt>("eval_consts", air.id == ZKP_AIR_MIMC ? (size_t)ce + 4 : 4 * (size_t)lw + 2);
+  launch_dt_eval_consts(pf, st, air.id, dt_cc, air.k, ec.w_last, dt_aval, dz, ce, w, air.num_t, dconst);
   ec.zinv = air.id == ZKP_AIR_MIMC ? dconst : dz;
   const std::string dom = std::to_string(logn) + "_" + std::to_string(logB) + "_" + std::to_string(u0) + "_" +
                           std::to_string(cel);
@@ -596,9 +596,7 @@ void constraint_eval(zkp_ctx* ctx, const AirDesc& air, uint32_t logn, uint32_t l
       ctx->upload(dk, kv.data(), kv.size() * 16);
     }
     MimcEvalArgs ma;
-    ma.bcoef = dconst + ce;  // b0, b1
-    ma.v0 = air.a_val[0];
-    ma.v1 = air.a_val[1];
+    ma.bcoef = dconst + ce;  // the regrouped boundary constants A, Bc, Cc, D
     ma.kper = dk;
     // divisor inverses depend only on the domain and the assertion steps: cache per config
     std::string key = "binv_mimc_" + dom;
@@ -1408,9 +1406,18 @@ void ProofRun::trace_stage(const zkp_felt* h_trace) {
     draw.method = o->batching_constraints;
     draw.ncoef = ncoef;
     draw.out = dt_cc;
+    // host channel with a late paired upload: the root is read after that upload is
+    // issued, so its PCIe time (the host thread blocks on a pageable copy) overlaps the
+    // trace tree instead of following the root read
+    const bool late_first = host_channel && late_h_trace && R == 1;
     coeffs_drawn = commit_rows(ctx, cm, 0, tlde, n, w, logB, logn, R > 1, "ttree", ttree, T.trace_root,
-                               /*fetch_root=*/host_channel, host_channel ? nullptr : &draw, nullptr,
+                               /*fetch_root=*/host_channel && !late_first, host_channel ? nullptr : &draw, nullptr,
                                gu_lazy_on ? &gu_lazy : nullptr);
+    if (late_first) {
+      late_pairs_upload();
+      ctx->download(T.trace_root, ttree.nodes + 8, 32);
+      memcpy(ttree.top[1].data(), T.trace_root, 32);
+    }
   }
   troot_d = R > 1 ? ttree.top_d + 8 : ttree.nodes + 8;  // sharded: the device-built top
   // the composition coefficients (drawn on the device from the trace root)

@@ -190,7 +190,7 @@ void launch_gather_full(Prof& prof, hipStream_t s, const FullGatherArgs& a, uint
 void launch_dt_draw_coeffs(Prof& prof, hipStream_t s, uint32_t* seed, const uint32_t* root, uint32_t method,
                            uint32_t ncoef, felt* cc);
 // coefficient-dependent constants of the eval kernels (layout in kernels.hip)
-void launch_dt_eval_consts(Prof& prof, hipStream_t s, int air, const felt* cc, felt k, const felt* aval,
+void launch_dt_eval_consts(Prof& prof, hipStream_t s, int air, const felt* cc, felt k, felt w_last, const felt* aval,
                            const felt* zinv, uint32_t ce, uint32_t w, uint32_t num_t, felt* out);
 // OOD frame -> reseeds -> DEEP coefficients gamma (w + C) and dk[2..4) = kz, kzg
 // (ood[2a + {0,1}] = array a at z, zg; dk[0..2) = z, zg already)
@@ -229,8 +229,7 @@ struct EvalCommon {
 };
 // MiMC: x' - (x + K)^7 ; boundary steps 0 and n-1 on column 0
 struct MimcEvalArgs {
-  const felt* bcoef;     // device: b0, b1 (boundary coefficients drawn on the device)
-  felt v0, v1;
+  const felt* bcoef;     // device: A, Bc, Cc, D of the regrouped boundary numerator (k_dt_eval_consts)
   const felt* kper;      // 64*ce periodic values on the CE domain
   felt* binv;            // scratch: one felt per 2048 CE points (per-block inverse products)
   felt* dinv;            // M felts: 1/((x - 1)(x - w^(n-1))) per CE point (domain-only, cached in the ctx)
