@@ -1,6 +1,6 @@
 #!/bin/bash
 # A/B of two libzkp builds on one box (tuning only): scripts/ab_libs.sh <lib A> <lib B> [bench args]
-# alternates A and B three times; prints ms_per_step, device_resident_ms, the dominant
+# alternates A and B three times; prints ms_per_step, pcie_inclusive ms, the dominant
 # kernel's live average launch and the per-kernel ms of the profiled proofs.
 set -o pipefail
 A=$1; B=$2; shift 2
@@ -10,7 +10,7 @@ for r in 1 2 3; do
     echo "$L $(echo "$out" | python -c '
 import json,sys
 d=json.loads(sys.stdin.readline()); k=d["launches"]["by_kernel_ms"]
-print(d["ms_per_step"], d["device_resident_ms"], d["roofline"]["kernel"], d["roofline"]["avg_launch_ms"],
+print(d["ms_per_step"], d["pcie_inclusive"]["ms_per_proof"], d["roofline"]["kernel"], d["roofline"]["avg_launch_ms"],
       " ".join(f"{n}={k[n]}" for n in list(k)[:8]))')"
   done
 done

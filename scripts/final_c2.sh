@@ -10,5 +10,5 @@ python3 -c "
 import json
 for f in ['b_c2','b_c3']:
     d=json.loads(open('gpurun_out/'+f+'.json').read().strip().splitlines()[-1])
-    print(f, d['value'], d['ms_per_step'], d['device_resident_ms'], d['roofline']['frac'], d['roofline']['avg_launch_ms'], d['launches']['per_proof'])
+    print(f, d['value'], d['ms_per_step'], d['pcie_inclusive']['ms_per_proof'], d['roofline']['frac'], d['roofline']['avg_launch_ms'], d['launches']['per_proof'])
 "

@@ -11,7 +11,7 @@ for r in 1 2; do
     echo "$L $(echo "$out" | python -c '
 import json,sys
 d=json.loads(sys.stdin.readline()); k=d["launches"]["by_kernel_ms"]
-print(d["ms_per_step"], d["device_resident_ms"], d["roofline"]["avg_launch_ms"], " ".join(f"{n}={k[n]}" for n in list(k)[:7]))')"
+print(d["ms_per_step"], d["pcie_inclusive"]["ms_per_proof"], d["roofline"]["avg_launch_ms"], " ".join(f"{n}={k[n]}" for n in list(k)[:7]))')"
   done
 done
 bash scripts/ab_valu.sh build_exp/b/x/libzkp.so zk_stark_project_amd/libzkp.so r3

@@ -13,7 +13,7 @@ timeout -k 10 400 python bench.py --steps 20 --no-cpu-baseline --sharded-leg > g
 python3 -c "
 import json
 d=json.loads(open('gpurun_out/b_c2s.json').read().strip().splitlines()[-1])
-print('C2', d['value'], d['ms_per_step'], d['device_resident_ms'], d['roofline']['frac'], d['roofline']['valu_floor_frac'])
+print('C2', d['value'], d['ms_per_step'], d['pcie_inclusive']['ms_per_proof'], d['roofline']['frac'], d['roofline']['valu_floor_frac'])
 print('session', d['session'])
 sh=d.get('sharded'); print('sharded', {k: sh[k] for k in sh if k not in ('fabric',)} if sh else None)
 "

@@ -12,6 +12,6 @@ python3 -c "
 import json
 for f in ('b_c2', 'b_c3'):
     d=json.loads(open('gpurun_out/%s.json' % f).read().strip().splitlines()[-1])
-    print(f, d['value'], d['ms_per_step'], d['device_resident_ms'], d['roofline']['frac'], d['roofline']['valu_floor_frac'])
+    print(f, d['value'], d['ms_per_step'], d['pcie_inclusive']['ms_per_proof'], d['roofline']['frac'], d['roofline']['valu_floor_frac'])
     print('  session', d['session']['session_ms'], d['session']['equals_zkp_prove_transcript'], d['session'].get('stage_ms'))
 "

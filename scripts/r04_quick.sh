@@ -14,6 +14,6 @@ timeout -k 10 300 python bench.py --steps 20 --no-cpu-baseline > gpurun_out/b_c2
 python3 -c "
 import json
 d=json.loads(open('gpurun_out/b_c2.json').read().strip().splitlines()[-1])
-print('C2', d['value'], d['ms_per_step'], d['device_resident_ms'], d['roofline']['frac'], d['roofline']['avg_launch_ms'])
+print('C2', d['value'], d['ms_per_step'], d['pcie_inclusive']['ms_per_proof'], d['roofline']['frac'], d['roofline']['avg_launch_ms'])
 print(d['launches']['by_kernel_ms'])
 "
