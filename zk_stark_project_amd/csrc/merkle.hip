@@ -1025,6 +1025,96 @@ __device__ __forceinline__ felt fri_fold_row(const felt* __restrict__ E, uint64_
   return mul(acc, eps_inv[8]);
 }
 
+// The same fold by a quad of lanes (the latency-bound small layers: one row's
+// 35 serial products become 19). Lane qd holds v[qd + 4i], i < 4: the iDFT's
+// span-8 and span-4 stages stay in the lane, the span-2 and span-1 stages pair
+// lanes qd^2 and qd^1 (DPP). Lane qd then holds u_k for k = 4*rev2(qd) + rev2(i),
+// evaluates its 4 coefficients by Horner, scales by beta^(4*rev2(qd)), and the
+// quad sums the four partials; every lane of the quad returns the folded value.
+// All 4 lanes of a quad must be active (callers clamp the row, not the lanes).
+template <int K>
+__device__ __forceinline__ felt quad_xor(felt v) {  // lane qd ^ K's value (K = 1 or 2)
+  constexpr int ctrl = K == 1 ? 0xB1 : 0x4E;  // quad_perm [1,0,3,2] / [2,3,0,1]
+  uint32_t w[4] = {(uint32_t)v.lo, (uint32_t)(v.lo >> 32), (uint32_t)v.hi, (uint32_t)(v.hi >> 32)};
+#pragma unroll
+  for (int i = 0; i < 4; i++) w[i] = (uint32_t)__builtin_amdgcn_mov_dpp((int)w[i], ctrl, 0xF, 0xF, false);
+  felt r;
+  r.lo = (uint64_t)w[0] | ((uint64_t)w[1] << 32);
+  r.hi = (uint64_t)w[2] | ((uint64_t)w[3] << 32);
+  return r;
+}
+
+__device__ __forceinline__ felt fri_fold_row_quad(const felt* __restrict__ E, uint64_t q, uint32_t qd, uint32_t logm16,
+                                                  uint32_t j0, uint32_t logB, const felt* alpha_p, felt off_inv,
+                                                  const felt* __restrict__ itw_lev,
+                                                  const felt* __restrict__ eps_inv) {
+  const uint64_t m16 = 1ull << logm16;
+  const uint64_t jl = q >> logm16, tp = q & (m16 - 1);
+  const uint64_t r = (j0 + jl) + (tp << logB);
+  const felt* src = E + (jl << (logm16 + 4)) + tp;
+  felt v[4];
+#pragma unroll
+  for (int i = 0; i < 4; i++) v[i] = src[(qd + 4 * i) * m16];
+  const felt beta = mul(*alpha_p, mul(off_inv, itw_lev[r]));
+  // span 8: pairs (qd, qd+8) = (v0, v2) and (qd+4, qd+12) = (v1, v3)
+  {
+    const felt a0 = add(v[0], v[2]), a1 = add(v[1], v[3]);
+    v[2] = mul(sub(v[0], v[2]), eps_inv[qd]);
+    v[3] = mul(sub(v[1], v[3]), eps_inv[qd + 4]);
+    v[0] = a0;
+    v[1] = a1;
+  }
+  // span 4 in each half: pairs (v0, v1) and (v2, v3), twiddle w^-(2 qd)
+  {
+    const felt e = eps_inv[2 * qd];
+    const felt a0 = add(v[0], v[1]), a2 = add(v[2], v[3]);
+    v[1] = mul(sub(v[0], v[1]), e);
+    v[3] = mul(sub(v[2], v[3]), e);
+    v[0] = a0;
+    v[2] = a2;
+  }
+  // span 2 (lanes qd, qd^2; position 3 of each 4-block takes w^-4), span 1 (lanes qd, qd^1)
+  const bool up2 = qd & 2, up1 = qd & 1;
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    const felt p = quad_xor<2>(v[i]);
+    v[i] = up2 ? sub(p, v[i]) : add(v[i], p);
+  }
+  if (qd == 3) {
+#pragma unroll
+    for (int i = 0; i < 4; i++) v[i] = mul(v[i], eps_inv[4]);
+  }
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    const felt p = quad_xor<1>(v[i]);
+    v[i] = up1 ? sub(p, v[i]) : add(v[i], p);
+  }
+  // v[i] = u_{4 rq + rev2(i)}, rq = rev2(qd): Horner over u_{4rq+3}, u_{4rq+2}, u_{4rq+1}, u_{4rq}
+  felt acc = add(mul(v[3], beta), v[1]);
+  acc = add(mul(acc, beta), v[2]);
+  acc = add(mul(acc, beta), v[0]);
+  const uint32_t rq = ((qd & 1) << 1) | (qd >> 1);
+  const felt b2 = mul(beta, beta), b4 = mul(b2, b2), b8 = mul(b4, b4), b12 = mul(b8, b4);
+  const felt sc = rq == 0 ? one() : (rq == 1 ? b4 : (rq == 2 ? b8 : b12));
+  acc = mul(acc, sc);
+  acc = add(acc, quad_xor<1>(acc));
+  acc = add(acc, quad_xor<2>(acc));
+  return mul(acc, eps_inv[8]);
+}
+
+// small layers (latency-bound): one quad per row
+__global__ __launch_bounds__(TPB) void k_fri_fold16_quad(const felt* __restrict__ E, uint64_t rows, uint32_t logm16,
+                                                         uint32_t j0, uint32_t logB, const felt* __restrict__ alpha_p,
+                                                         felt off_inv, const felt* __restrict__ itw_lev,
+                                                         const felt* __restrict__ eps_inv, felt* __restrict__ out) {
+  const uint64_t tq = blockIdx.x * (uint64_t)TPB + threadIdx.x;
+  const uint64_t q = tq >> 2;
+  const uint32_t qd = (uint32_t)(tq & 3);
+  const felt v = fri_fold_row_quad(E, q < rows ? q : rows - 1, qd, logm16, j0, logB, alpha_p, off_inv, itw_lev,
+                                   eps_inv);  // whole quads active; clamped rows are not stored
+  if (q < rows && qd == 0) out[q] = v;
+}
+
 __global__ __launch_bounds__(TPB) void k_fri_fold16(const felt* __restrict__ E, uint64_t rows, uint32_t logm16,
                                                     uint32_t j0, uint32_t logB, const felt* __restrict__ alpha_p,
                                                     felt off_inv,
@@ -1090,7 +1180,11 @@ __global__ __launch_bounds__(512) void k_fri_tail(FriTailArgs a) {
     }
     __threadfence();  // alpha (and this layer's fold output below) visible block-wide
     __syncthreads();
-    if (t < R) y.out[t] = fri_fold_row(y.E, t, y.logm16, 0, a.logB, y.alpha_out, y.off_inv, y.lev, a.eps_inv);
+    {  // one quad per row (R <= 128 rows, 128 quads): whole quads active, rows clamped
+      const felt fv = fri_fold_row_quad(y.E, nd < R ? nd : R - 1, q, y.logm16, 0, a.logB, y.alpha_out, y.off_inv,
+                                        y.lev, a.eps_inv);
+      if (nd < R && q == 0) y.out[nd] = fv;
+    }
     __threadfence();
     __syncthreads();
   }
@@ -1317,6 +1411,14 @@ void launch_fri_fold(Prof& prof, hipStream_t s, const felt* E, uint64_t m16, uin
   uint32_t logm16 = 0;
   while ((1ull << logm16) < m16) logm16++;
   const uint64_t rows = m16 * Bl;
+  // up to 2^15 rows the layer is latency-bound (under one wave per SIMD): a quad
+  // per row shortens the chain; above that the one-lane form issues fewer products
+  if (rows <= (1ull << 15)) {
+    LAUNCH(prof, "fri_fold16", s, (double)rows * (16 * 16.0 + 16.0),
+           hipLaunchKernelGGL(k_fri_fold16_quad, dim3(blocks_for(rows * 4)), dim3(TPB), 0, s, E, rows, logm16, j0,
+                              logB, alpha, off_inv, lev, eps_inv, out));
+    return;
+  }
   LAUNCH(prof, "fri_fold16", s, (double)rows * (16 * 16.0 + 16.0),
          hipLaunchKernelGGL(k_fri_fold16, dim3(blocks_for(rows)), dim3(TPB), 0, s, E, rows, logm16, j0, logB, alpha,
                             off_inv, lev, eps_inv, out));
