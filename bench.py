@@ -292,6 +292,8 @@ def parse():
     ap.add_argument("--sharded-leg", action="store_true",
                     help="run the C4 sharded leg at N = 1 too (a world-1 RCCL rehearsal of its collectives and checks)")
     ap.add_argument("--stats", action="store_true", help="print the per-kernel table to stderr")
+    ap.add_argument("--no-concurrent", dest="concurrent", action="store_false",
+                    help="N=1: skip the leg with 3 proofs in flight on the GPU")
     ap.add_argument("--air", choices=["mimc", "agg"], default="mimc",
                     help="mimc = C2 (default, the BASELINE metric); agg = C3 GlobalUpdate (64 updates, 2^18 rows)")
     return ap.parse_args()
@@ -424,6 +426,51 @@ def session_leg(ctx, wl, pub, tr, steps: int) -> dict:
                      "zkp_deep_fri -> zkp_grind -> zkp_query, coefficients from zkp_channel (host)"}
 
 
+def concurrent_leg(wl, pub, want: bytes, in_flight: int = 3, seconds: float = 1.5) -> dict:
+    """Proofs/s on this GPU with `in_flight` proofs at once: that many host threads,
+    each with its own zkp_ctx (own streams and HBM buffers) and its own copy of the
+    trace in HBM, proving back to back (ctypes drops the GIL inside zkp_prove_device).
+    One proof's latency-bound phases (tree tops, FRI tail, coin steps, grinding's
+    search end) then overlap another's bandwidth-bound kernels. Reported beside the
+    headline, which keeps one proof in flight."""
+    from zk_stark_project_amd import _native
+    ctxs = [_native.Context(0) for _ in range(in_flight)]
+    host = wl["trace"].data
+    dts = []
+    for c in ctxs:
+        d = c.alloc(host.nbytes)
+        c.to_device(d, host)
+        dts.append(d)
+    same = True
+    for c, d in zip(ctxs, dts):  # warm: each context's domain tables
+        p, _ = c.prove_device(wl["air_id"], d, wl["width"], wl["n"], pub, wl["opts"])
+        same = same and p == want
+    counts = [0] * in_flight
+    stop = threading.Event()
+
+    def worker(i):
+        nonlocal same
+        while not stop.is_set():
+            p, _ = ctxs[i].prove_device(wl["air_id"], dts[i], wl["width"], wl["n"], pub, wl["opts"])
+            same = same and p == want
+            counts[i] += 1
+    th = [threading.Thread(target=worker, args=(i,)) for i in range(in_flight)]
+    t0 = time.perf_counter()
+    for t in th:
+        t.start()
+    time.sleep(seconds)
+    stop.set()
+    for t in th:
+        t.join()
+    dt = time.perf_counter() - t0
+    total = sum(counts)
+    return {"in_flight": in_flight, "proofs": total, "seconds": round(dt, 3),
+            "proofs_per_s": round(total / dt, 3), "ms_per_proof_amortized": round(dt / total * 1e3, 3),
+            "latency_ms_per_proof": round(dt / max(1, min(counts)) * 1e3, 3),
+            "proof_bytes_identical": same,
+            "step": "zkp_prove_device from HBM, one zkp_ctx and host thread per proof in flight"}
+
+
 def sharded_self_check(ctx, wl, pub, proof, rank: int, world: int, dist, local_rank: int) -> dict:
     """After the timed sharded proofs (outside the timed region): every rank checks its
     last proof with the product verifier (zkp_verify) and hashes its bytes; rank 0 also
@@ -552,6 +599,8 @@ def main():
     # the stage-hook route (a winter-prover fork keeping Prover::prove): the same proof
     # through zkp_session_* with the host channel drawing every coefficient
     session = None if sharded else session_leg(ctx, wl, pub, tr, min(args.steps, 10))
+    # several proofs in flight on this one GPU (a proof service's throughput)
+    concurrent = concurrent_leg(wl, pub, proof) if (world == 1 and not sharded and args.concurrent) else None
     # the oracle's verifier (CPU) runs after every timed region, so the GPU does not
     # sit idle (and clock down) just before the timed steps
     verified = None
@@ -693,6 +742,7 @@ def main():
                      "(SURVEY.md §8(d) 'prove')")},
         "first_proof_ms": round(first_ms, 3),
         "sustained": {"proofs": sus_n, "seconds": round(sus_s, 3), "proofs_per_s": round(sus_n / sus_s, 3)},
+        "concurrent": concurrent,
         "session": ({**session, "over_pcie_inclusive": round(session["session_ms"] / (el_in / args.steps * 1e3), 3)}
                     if session and headline is not prove_once else session),
         "roofline": roofline,
