@@ -6,13 +6,18 @@ trace, 1/2/4/8 MI355X". Workload = BASELINE.json configs[1]:
 MiMC AIR, n = 2^20, x0 = 42e6, ProofOptions(40, 8, 21,
 None, 16, 7, Algebraic, Algebraic).
 
-A "step" is one proof with its input already resident in HBM when the timed
-region starts: `zkp_prove_device`, trace in HBM -> serialized proof bytes on the
-host. `value` = proofs/s and `ms_per_step` = ms/proof of those calls. Extra
-keys: `pcie_inclusive` (the same proof by `zkp_prove` from the pageable host
-trace, upload over PCIe included: SURVEY.md §8(d)'s "prove"; never `value`),
-`first_proof_ms` (first proof of a fresh context: domain tables built cold),
-`sustained` (proofs/s over a few seconds).
+A "step" is SURVEY.md §8(d)'s "prove": `zkp_prove` wall-clock from the host
+trace (a pageable numpy array, built before timing) to the serialized proof
+bytes, PCIe upload included. `value` = proofs/s and `ms_per_step` = mean
+ms/proof of those calls; `step_ms` gives their median and min (BASELINE.md:35).
+Extra keys: `trace_resident` (the same proof by `zkp_prove_device` with the
+trace already in HBM; never `value`), `first_proof_ms` (first proof of a
+fresh context: domain tables built cold), `sustained` (proofs/s over a few
+seconds), `c3` (BASELINE configs[2]: the aggregation AIR, 64 updates, 2^18 x
+120, reference options, with its own roofline and oracle byte check) and
+`reference_flow` (/root/reference/src/main.rs:374-493, the reference binary's
+proof step: 8 TrainingUpdate proofs at bs = 50 and the GlobalUpdate proof,
+cold and warm, beside the oracle).
 
 Multi-GPU: one process per GPU (torchrun). Default `--mode replicas`: each
 rank proves its own independent 2^20 trace on its own device (weak scaling,
@@ -294,6 +299,10 @@ def parse():
     ap.add_argument("--stats", action="store_true", help="print the per-kernel table to stderr")
     ap.add_argument("--no-concurrent", dest="concurrent", action="store_false",
                     help="N=1: skip the leg with 3 proofs in flight on the GPU")
+    ap.add_argument("--no-c3", dest="c3", action="store_false",
+                    help="N=1 MiMC line: skip the C3 leg (BASELINE configs[2])")
+    ap.add_argument("--no-reference-flow", dest="reference_flow", action="store_false",
+                    help="N=1 MiMC line: skip the reference binary's proof step (main.rs:374-493)")
     ap.add_argument("--air", choices=["mimc", "agg"], default="mimc",
                     help="mimc = C2 (default, the BASELINE metric); agg = C3 GlobalUpdate (64 updates, 2^18 rows)")
     return ap.parse_args()
@@ -496,6 +505,225 @@ def sharded_self_check(ctx, wl, pub, proof, rank: int, world: int, dist, local_r
             "self_check": "zkp_verify on every rank; rank 0's world-1 zkp_prove of the same trace vs the sharded "
                           "bytes; every rank's proof hash all-gathered"}
 
+def measure(ctx, headline, steps: int, warmup: int, dist=None, sync=None, device=None) -> dict:
+    """One workload's timing: the first proof of a fresh shape (domain tables built cold),
+    two untimed proofs with every launch bracketed by HIP events (the per-kernel table,
+    which names the dominant kernel), the rest of the warm-up, then `steps` timed proofs
+    in which only the dominant kernel's launches carry events (its roofline is measured
+    live at ~no event overhead)."""
+    from zk_stark_project_amd.replicas import timed_replicas
+    t0 = time.perf_counter()
+    headline()
+    first_ms = (time.perf_counter() - t0) * 1e3
+    ctx.reset_stats()
+    ctx.set_profiling(True)
+    for _ in range(2):
+        headline()
+    ctx.set_profiling(False)
+    kernels = {k: v for k, v in ctx.stats_table().items() if not k.startswith("host_")}
+    dom_name = max(kernels.items(), key=lambda kv: kv[1]["ms"])[0]
+    for _ in range(max(warmup - 1, 0)):  # the rest of the W warm-up steps (the first proof was one)
+        headline()
+    ctx.reset_stats()
+    ctx.set_profiling(True, kernel=dom_name)
+    times = []
+    elapsed, _, (proof, tr) = timed_replicas(headline, steps, 0, dist=dist, device_sync=sync, device=device,
+                                              times=times)
+    ctx.set_profiling(False)
+    return {"first_ms": first_ms, "kernels": kernels, "dom_name": dom_name, "elapsed": elapsed, "times": times,
+            "proof": proof, "tr": tr, "stats": ctx.stats_table()}
+
+
+def step_summary(times) -> dict:
+    """Per-step wall times of the timed region (ms): mean, median, min, max."""
+    ts = sorted(t * 1e3 for t in times)
+    k = len(ts)
+    med = ts[k // 2] if k % 2 else (ts[k // 2 - 1] + ts[k // 2]) / 2
+    return {"mean": round(sum(ts) / k, 3), "median": round(med, 3), "min": round(ts[0], 3),
+            "max": round(ts[-1], 3), "n": k}
+
+
+def launches_of(kernels: dict) -> dict:
+    """Every launch of the two profiled proofs (HIP events per launch, side stream included)."""
+    total_ms = sum(v["ms"] for v in kernels.values())
+    return {"per_proof": sum(v["launches"] for v in kernels.values()) / 2,
+            "kernel_ms_per_proof": round(total_ms / 2, 3),
+            "by_kernel_ms": {k: round(v["ms"] / 2, 4) for k, v in sorted(kernels.items(), key=lambda kv: -kv[1]["ms"])}}
+
+
+def roofline_of(m: dict, wl: dict, R: int, steps: int, ms: float, air: str, mode: str) -> dict:
+    """The dominant kernel's roofline: SURVEY.md §8(d) algorithmic bytes per launch ÷ its
+    average HIP-event duration in the timed region; PMC traffic and VALU issue from the
+    committed summaries of the same workload; the NTT's butterfly floor."""
+    kernels, stats, dom_name = m["kernels"], m["stats"], m["dom_name"]
+    B, n = wl["opts"].blowup_factor, wl["n"]
+    sb = stage_bytes(wl["width"], n, B, wl["ce"], wl["C"])
+    bytes_per_proof = sum(sb.values())
+    total_ms = sum(v["ms"] for v in kernels.values())
+    dom = stats[dom_name]  # HIP events of the timed region
+    dom_avg_ms = dom["ms"] / dom["launches"]
+    launches_per_proof = dom["launches"] / steps
+    kbytes, ksrc = kernel_stage_bytes(dom_name, sb, wl, R)
+    alg = kbytes / R / launches_per_proof if kbytes else None
+    # the NTT's butterfly floor: butterflies of the extended columns' coset NTTs at the
+    # micro-benchmark's register-resident rate, against the kernel's time per proof
+    valu_floor = None
+    if dom_name == "ntt_dit" and floor_rate():
+        tcols, ccols = lde_columns(wl, R)
+        bfly = (tcols + ccols) * B / R * (n // 2) * wl["log_n"]
+        kernel_ms = dom_avg_ms * launches_per_proof
+        floor_ms = bfly / (floor_rate() * 1e9) * 1e3
+        valu_floor = {"butterflies_per_proof": bfly, "floor_gbfly_per_s": floor_rate(), "floor_ms": round(floor_ms, 4),
+                      "kernel_ms_per_proof": round(kernel_ms, 4), "valu_floor_frac": round(floor_ms / kernel_ms, 3),
+                      "source": f"{UBENCH_BFLY} (tests/native/ubench_bfly.hip, the library's butterfly forms)"}
+    traffic, traffic_src = pmc_traffic(dom_name, air, mode)
+    return {
+        "bound": "hbm",
+        "kernel": dom_name,
+        "achieved": round(alg / (dom_avg_ms * 1e-3) / 1e9, 2) if alg else None,
+        "peak": HBM_PEAK_GBS,
+        "unit": "GB/s",
+        "frac": round(alg / (dom_avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if alg else None,
+        "traffic": traffic,
+        "traffic_source": traffic_src,
+        "algorithmic_bytes_per_launch": alg,
+        "algorithmic_bytes_source": (f"SURVEY.md §8(d)/Appendix C {ksrc} = {kbytes} B per proof / "
+                                     f"{launches_per_proof:g} launches" if kbytes else None),
+        "traffic_over_algorithmic": round(traffic / alg, 2) if traffic and alg else None,
+        "traffic_model_per_launch": dom["bytes"] / dom["launches"],
+        "avg_launch_ms": round(dom_avg_ms, 5),
+        "launches_per_proof": launches_per_proof,
+        "share_of_device_time": round(kernels[dom_name]["ms"] / total_ms, 3) if total_ms else None,
+        "whole_proof_frac": round(bytes_per_proof / R / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+        "bytes_per_proof_8d": bytes_per_proof,
+        "valu": valu_side(dom_name, air, mode),
+        "valu_floor_frac": valu_floor["valu_floor_frac"] if valu_floor else None,
+        "valu_floor": valu_floor,
+    }
+
+
+def c3_leg(ctx, steps: int, warmup: int, check: bool) -> dict:
+    """BASELINE configs[2] / SURVEY §8(d) C3 on the same GPU: the GlobalUpdate AIR over 64
+    device updates padded to 2^18 rows x 120 columns (/root/reference/src/aggregation/
+    prover.rs:98-160), the reference's options (src/main.rs:98-107: 40, 16, 21, None, 16,
+    7, Algebraic, Algebraic). Same step as the headline (zkp_prove from the host trace),
+    its own roofline, and — after the timed region — the proof checked byte for byte
+    against the C oracle's proof of the same trace."""
+    wl = make_workload("agg", False, None, 16, 0, ctx)
+    pub = wl["prover"].get_pub_inputs(wl["trace"]).to_elements()
+    host = wl["trace"].data
+    d_tr = ctx.alloc(host.nbytes)
+    ctx.to_device(d_tr, host)
+    try:
+        m = measure(ctx, lambda: ctx.prove(wl["air_id"], host, pub, wl["opts"]), steps, warmup)
+        el_in, _, _ = timed_replicas_plain(
+            lambda: ctx.prove_device(wl["air_id"], d_tr, wl["width"], wl["n"], pub, wl["opts"]), steps)
+    finally:
+        ctx.free(d_tr)
+    ms = m["elapsed"] / steps * 1e3
+    out = {"workload": wl["workload"], "options": "(40, 16, 21, None, 16, 7, Algebraic, Algebraic) (src/main.rs:98-107)",
+           "value": round(steps / m["elapsed"], 3), "unit": "proofs/s", "ms_per_step": round(ms, 3),
+           "steps": steps, "step_ms": step_summary(m["times"]),
+           "step": "zkp_prove: host trace (pageable numpy) -> proof bytes, PCIe upload included",
+           "trace_resident": {"ms_per_proof": round(el_in / steps * 1e3, 3), "proofs_per_s": round(steps / el_in, 3)},
+           "first_proof_ms": round(m["first_ms"], 3),
+           "roofline": roofline_of(m, wl, 1, steps, ms, "agg", "replicas"),
+           "launches": launches_of(m["kernels"]), "proof_bytes": len(m["proof"])}
+    if check:
+        import oracle_ref
+        t0 = time.perf_counter()
+        ref, _ = oracle_ref.prove(wl["air_id"], wl["trace"].to_bytes(), wl["width"], wl["n"],
+                                  b"".join(v.to_bytes(16, "little") for v in pub), wl["opts"])
+        out["oracle_ms"] = round((time.perf_counter() - t0) * 1e3, 1)
+        out["oracle_threads"] = oracle_ref.lib().oracle_num_threads()
+        out["proof_bytes_identical"] = ref == m["proof"]
+    return out
+
+
+def timed_replicas_plain(fn, steps: int):
+    """`steps` back-to-back calls after one warm-up call (single rank): (elapsed, None, last)."""
+    from zk_stark_project_amd.replicas import timed_replicas
+    return timed_replicas(fn, steps, 1)
+
+
+REF_FLOW_DEVICES, REF_FLOW_BS = 8, 50
+
+
+def reference_flow_leg(device: int, check: bool) -> dict:
+    """The reference binary's proof step (/root/reference/src/main.rs:374-493, `--step proof
+    --bs 50`): one TrainingUpdate proof per device (bs = 50 samples: n = 8192 rows, w = 240,
+    src/training/prover.rs:63), each verified, then the GlobalUpdate proof over the
+    devices' last-row values (8 updates: n = 16), verified; the reference's options
+    (src/main.rs:98-107, blowup 16). The harness (verification/time_memory_analytics/
+    analyze.py:476-482) reads the aggregation's "proof: Tms".
+
+    Timed on a FRESH zkp_ctx — every shape's domain tables and buffers built on first use,
+    as the reference's fresh process does — (`cold`), then again on the same context
+    (`warm`). The 8 synthetic devices hold 60 seeded rows of 9 features + a label
+    (the Device_* CSV layout, helper.rs:55-80). Traces are built once beforehand by the
+    host mirror of the trace builders (Python; `trace_build_ms`), outside the proof
+    timings, like the reference times `proof:` apart from `trace:`. With `check`, every
+    proof is compared with the C oracle's proof of the same trace (`oracle_ms` per proof)."""
+    import random
+    from zk_stark_project_amd import AIR_GLOBAL_UPDATE, AIR_TRAINING_UPDATE, _native, cli
+    from zk_stark_project_amd.helper import FE, EdgeDevice
+    from zk_stark_project_amd.options import ProofOptions
+    opts = ProofOptions.reference()
+    rng, drng = random.Random(2024), random.Random(99)
+    devs = [EdgeDevice([[drng.uniform(-2, 2) for _ in range(FE)] for _ in range(60)],
+                       [float(drng.randrange(1, 9)) for _ in range(60)], random.Random(rng.getrandbits(64)))
+            for _ in range(REF_FLOW_DEVICES)]
+    t0 = time.perf_counter()
+    jobs = []
+    for d in devs:
+        tp = cli._training_prover(opts, cli._zk_batch(d, REF_FLOW_BS), REF_FLOW_BS, rng, None)
+        tr = tp.build_trace()
+        jobs.append((AIR_TRAINING_UPDATE, tr, tp.get_pub_inputs(tr).to_elements()))
+    agg = cli._aggregator(opts, [tr.get(0, tr.length() - 1) for _, tr, _ in jobs], rng, None)
+    agg_tr = agg.build_trace()
+    jobs.append((AIR_GLOBAL_UPDATE, agg_tr, agg.get_pub_inputs(agg_tr).to_elements()))
+    build_ms = (time.perf_counter() - t0) * 1e3
+
+    def run(ctx):
+        proofs, prove_ms = [], []
+        t_all = time.perf_counter()
+        for air, tr, pub in jobs:
+            t1 = time.perf_counter()
+            p, _ = ctx.prove(air, tr.data, pub, opts)
+            prove_ms.append((time.perf_counter() - t1) * 1e3)
+            _native.verify(air, p, pub, opts)  # main.rs:430-436, 478-484 (zkp_verify, host)
+            proofs.append(p)
+        total = (time.perf_counter() - t_all) * 1e3
+        return proofs, {"training_proof_ms": [round(x, 3) for x in prove_ms[:-1]],
+                        "aggregation_proof_ms": round(prove_ms[-1], 3),
+                        "prove_ms_total": round(sum(prove_ms), 3), "flow_ms": round(total, 3)}
+
+    ctx = _native.Context(device)
+    try:
+        proofs, cold = run(ctx)
+        proofs2, warm = run(ctx)
+    finally:
+        ctx.close()
+    out = {"workload": f"src/main.rs:374-493 --step proof --bs {REF_FLOW_BS}: {REF_FLOW_DEVICES} TrainingUpdate proofs "
+                       f"(n = {jobs[0][1].length()}, w = {jobs[0][1].width()}) + GlobalUpdate proof "
+                       f"(n = {agg_tr.length()}, w = {agg_tr.width()}), blowup 16, each verified",
+           "cold": cold, "warm": warm, "trace_build_ms": round(build_ms, 1),
+           "cold_context": "fresh zkp_ctx: domain tables, twiddles and buffers built on first use of each shape",
+           "proof_bytes": [len(p) for p in proofs], "warm_equals_cold": proofs == proofs2}
+    if check:
+        import oracle_ref
+        ms, same = [], True
+        for (air, tr, pub), p in zip(jobs, proofs):
+            t1 = time.perf_counter()
+            ref, _ = oracle_ref.prove(air, tr.to_bytes(), tr.width(), tr.length(),
+                                      b"".join(v.to_bytes(16, "little") for v in pub), opts)
+            ms.append(round((time.perf_counter() - t1) * 1e3, 1))
+            same = same and ref == p
+        out["oracle"] = {"training_proof_ms": ms[:-1], "aggregation_proof_ms": ms[-1], "prove_ms_total": round(sum(ms), 1),
+                         "threads": oracle_ref.lib().oracle_num_threads()}
+        out["proof_bytes_identical"] = same
+    return out
+
 
 def main():
     args = parse()
@@ -557,40 +785,17 @@ def main():
         def prove_dev():  # zkp_prove_device: trace resident in HBM
             return ctx.prove_device(air_id, d_trace, width, n, pub, opts)
 
-    # the headline step: input resident in HBM (the C5 step builds its trace on the
-    # device from the updates first: that build is part of the sharded C5 step)
-    headline = prove_once if (sharded and args.air == "agg") else prove_dev
-    # first proof of a fresh context: twiddles, coset scales and divisor tables built cold
-    t0 = time.perf_counter()
-    proof, _ = headline()
-    first_ms = (time.perf_counter() - t0) * 1e3
-    # per-kernel table from two untimed proofs with every launch bracketed; it
-    # names the dominant kernel, whose launches alone carry HIP events in the
-    # timed region (so the roofline is measured live at ~no event overhead)
-    ctx.reset_stats()
-    ctx.set_profiling(True)
-    for _ in range(2):
-        headline()
-    ctx.set_profiling(False)
-    full_stats = ctx.stats_table()
-    kernels = {k: v for k, v in full_stats.items() if not k.startswith("host_")}
-    dom_name = max(kernels.items(), key=lambda kv: kv[1]["ms"])[0]
-    for _ in range(max(args.warmup - 1, 0)):  # the rest of the W warm-up steps (the first proof was one)
-        headline()
-    ctx.reset_stats()
-    ctx.set_profiling(True, kernel=dom_name)  # only the timed proofs carry events
-    elapsed, _, (proof, tr) = timed_replicas(headline, args.steps, 0, dist=dist,
-                                              device_sync=cuda_sync if dist is not None else None,
-                                              device=f"cuda:{local_rank}")
-    ctx.set_profiling(False)
-    stats = ctx.stats_table()
-    # the same proof from the pageable host trace, PCIe upload included (zkp_prove;
-    # SURVEY.md §8(d)'s "prove"): reported beside the headline, never as `value`
-    # (C5: the trace already in HBM, without the device build)
-    second = prove_dev if headline is prove_once else prove_once
-    el_in, _, _ = timed_replicas(second, args.steps, 1, dist=dist,
-                                 device_sync=cuda_sync if dist is not None else None, device=f"cuda:{local_rank}")
-    # sustained: back-to-back proofs for a few seconds (clock / thermal steadiness)
+    # the headline step: SURVEY.md §8(d)'s "prove" — zkp_prove from the host trace,
+    # uploads included (C5: the trace built on every rank's device from the updates,
+    # then the sharded proof); the trace-resident proof is reported beside it
+    headline, second = prove_once, prove_dev
+    sync = cuda_sync if dist is not None else None
+    m = measure(ctx, headline, args.steps, args.warmup, dist=dist, sync=sync, device=f"cuda:{local_rank}")
+    elapsed, proof, tr, kernels, dom_name = m["elapsed"], m["proof"], m["tr"], m["kernels"], m["dom_name"]
+    # the same proof with the trace already in HBM (zkp_prove_device / a device-resident
+    # sharded proof): reported beside the headline, never as `value`
+    el_in, _, _ = timed_replicas(second, args.steps, 1, dist=dist, device_sync=sync, device=f"cuda:{local_rank}")
+    # sustained: back-to-back headline proofs for a few seconds (clock / thermal steadiness)
     sus_n, t1 = 0, time.perf_counter()
     while time.perf_counter() - t1 < args.sustain_s:
         headline()
@@ -601,6 +806,14 @@ def main():
     session = None if sharded else session_leg(ctx, wl, pub, tr, min(args.steps, 10))
     # several proofs in flight on this one GPU (a proof service's throughput)
     concurrent = concurrent_leg(wl, pub, proof) if (world == 1 and not sharded and args.concurrent) else None
+    # BASELINE configs[2] (C3) on the same GPU, and the reference binary's own proof step
+    if world == 1 and not args.no_verify:
+        import oracle_ref  # their byte checks run the oracle on every CPU of this job's host share
+        oracle_ref.lib().oracle_set_threads(host_cpus())
+    c3 = c3_leg(ctx, args.steps, args.warmup, not args.no_verify) if (
+        world == 1 and not sharded and args.air == "mimc" and args.c3) else None
+    ref_flow = reference_flow_leg(local_rank, not args.no_verify) if (
+        world == 1 and not sharded and args.air == "mimc" and args.reference_flow) else None
     # the oracle's verifier (CPU) runs after every timed region, so the GPU does not
     # sit idle (and clock down) just before the timed steps
     verified = None
@@ -626,53 +839,11 @@ def main():
             sys.exit(1)
         return
 
-    B = opts.blowup_factor
     R = world if sharded else 1
-    sb = stage_bytes(width, n, B, wl["ce"], wl["C"])
-    bytes_per_proof = sum(sb.values())
-    host_stages = {k: v for k, v in stats.items() if k.startswith("host_")}
-    total_ms = sum(v["ms"] for v in kernels.values())
-    dom = stats[dom_name]  # HIP events of the timed region
-    dom_avg_ms = dom["ms"] / dom["launches"]
-    launches_per_proof = dom["launches"] / args.steps
-    kbytes, ksrc = kernel_stage_bytes(dom_name, sb, wl, R)
-    alg = kbytes / R / launches_per_proof if kbytes else None
-    # the NTT's butterfly floor: butterflies of the extended columns' coset NTTs at the
-    # micro-benchmark's register-resident rate, against the kernel's time per proof
-    valu_floor = None
-    if dom_name == "ntt_dit" and floor_rate():
-        tcols, ccols = lde_columns(wl, R)
-        bfly = (tcols + ccols) * B / R * (n // 2) * wl["log_n"]
-        kernel_ms = dom_avg_ms * launches_per_proof
-        floor_ms = bfly / (floor_rate() * 1e9) * 1e3
-        valu_floor = {"butterflies_per_proof": bfly, "floor_gbfly_per_s": floor_rate(), "floor_ms": round(floor_ms, 4),
-                      "kernel_ms_per_proof": round(kernel_ms, 4), "valu_floor_frac": round(floor_ms / kernel_ms, 3),
-                      "source": f"{UBENCH_BFLY} (tests/native/ubench_bfly.hip, the library's butterfly forms)"}
-    traffic, traffic_src = pmc_traffic(dom_name, args.air, args.mode)
+    B = opts.blowup_factor
+    host_stages = {k: v for k, v in m["stats"].items() if k.startswith("host_")}
     ms = elapsed / args.steps * 1e3
-    roofline = {
-        "bound": "hbm",
-        "kernel": dom_name,
-        "achieved": round(alg / (dom_avg_ms * 1e-3) / 1e9, 2) if alg else None,
-        "peak": HBM_PEAK_GBS,
-        "unit": "GB/s",
-        "frac": round(alg / (dom_avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if alg else None,
-        "traffic": traffic,
-        "traffic_source": traffic_src,
-        "algorithmic_bytes_per_launch": alg,
-        "algorithmic_bytes_source": (f"SURVEY.md §8(d)/Appendix C {ksrc} = {kbytes} B per proof / "
-                                     f"{launches_per_proof:g} launches" if kbytes else None),
-        "traffic_over_algorithmic": round(traffic / alg, 2) if traffic and alg else None,
-        "traffic_model_per_launch": dom["bytes"] / dom["launches"],
-        "avg_launch_ms": round(dom_avg_ms, 5),
-        "launches_per_proof": launches_per_proof,
-        "share_of_device_time": round(kernels[dom_name]["ms"] / total_ms, 3) if total_ms else None,
-        "whole_proof_frac": round(bytes_per_proof / R / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-        "bytes_per_proof_8d": bytes_per_proof,
-        "valu": valu_side(dom_name, args.air, args.mode),
-        "valu_floor_frac": valu_floor["valu_floor_frac"] if valu_floor else None,
-        "valu_floor": valu_floor,
-    }
+    roofline = roofline_of(m, wl, R, args.steps, ms, args.air, args.mode)
 
     cpu = None
     c1 = None
@@ -731,28 +902,26 @@ def main():
                    "env": zkp_env(),
                    "step": ("GlobalUpdate trace built on each rank's device from the updates + zkp_prove_sharded"
                             if sharded and args.air == "agg" else
-                            "zkp_prove_sharded: trace resident in every rank's HBM -> proof bytes" if sharded else
-                            "zkp_prove_device: trace resident in HBM -> proof bytes on the host")},
-        ("trace_resident" if headline is prove_once else "pcie_inclusive"): {
+                            "zkp_prove_sharded from the host trace: each rank uploads its row slice" if sharded else
+                            "zkp_prove: host trace (pageable numpy) -> proof bytes, PCIe upload included "
+                            "(SURVEY.md §8(d) 'prove')")},
+        "step_ms": step_summary(m["times"]),
+        "trace_resident": {
             "ms_per_proof": round(el_in / args.steps * 1e3, 3),
             "proofs_per_s": round(aggregate_rate(1 if sharded else world, args.steps, el_in), 3),
-            "step": ("zkp_prove_sharded on a trace already in HBM (no device build)" if headline is prove_once else
-                     "zkp_prove_sharded from the host trace: each rank uploads its row slice" if sharded else
-                     "zkp_prove: host trace (pageable numpy) -> proof bytes, PCIe upload included "
-                     "(SURVEY.md §8(d) 'prove')")},
-        "first_proof_ms": round(first_ms, 3),
+            "step": ("zkp_prove_sharded on a trace already in every rank's HBM" if sharded else
+                     "zkp_prove_device: trace resident in HBM -> proof bytes on the host")},
+        "first_proof_ms": round(m["first_ms"], 3),
         "sustained": {"proofs": sus_n, "seconds": round(sus_s, 3), "proofs_per_s": round(sus_n / sus_s, 3)},
         "concurrent": concurrent,
-        "session": ({**session, "over_pcie_inclusive": round(session["session_ms"] / (el_in / args.steps * 1e3), 3)}
-                    if session and headline is not prove_once else session),
+        "session": ({**session, "over_zkp_prove": round(session["session_ms"] / ms, 3)} if session else None),
         "roofline": roofline,
         # every launch of the two profiled proofs (HIP events per launch, side stream included)
-        "launches": {"per_proof": sum(v["launches"] for v in kernels.values()) / 2,
-                     "kernel_ms_per_proof": round(total_ms / 2, 3),
-                     "by_kernel_ms": {k: round(v["ms"] / 2, 4) for k, v in
-                                      sorted(kernels.items(), key=lambda kv: -kv[1]["ms"])}},
+        "launches": launches_of(kernels),
         "cpu_baseline": cpu,
         "c1": c1,
+        "c3": c3,
+        "reference_flow": ref_flow,
         "proof_bytes": len(proof),
         "verified_by_oracle": verified,
         "parity": "bit-exact vs the C oracle; parity vs winterfell 0.12 bytes unpinned (DESIGN.md §2)",

@@ -8,11 +8,13 @@ from __future__ import annotations
 import time
 
 
-def timed_replicas(prove_once, steps: int, warmup: int, dist=None, device_sync=None, device=None):
+def timed_replicas(prove_once, steps: int, warmup: int, dist=None, device_sync=None, device=None, times=None):
     """Run `warmup` untimed and `steps` timed calls of prove_once() on this rank.
 
     Timed region: barrier + device sync on both sides. Returns
-    (max_elapsed_over_ranks, local_elapsed, last_result)."""
+    (max_elapsed_over_ranks, local_elapsed, last_result). `times`: a list that
+    receives each timed call's own wall time in seconds (prove_once returns
+    host bytes, so a call ends when its proof is on the host)."""
     result = None
     for _ in range(warmup):
         result = prove_once()
@@ -22,7 +24,10 @@ def timed_replicas(prove_once, steps: int, warmup: int, dist=None, device_sync=N
         device_sync()
     t0 = time.perf_counter()
     for _ in range(steps):
+        t1 = time.perf_counter()
         result = prove_once()
+        if times is not None:
+            times.append(time.perf_counter() - t1)
     if device_sync is not None:
         device_sync()
     if dist is not None:
