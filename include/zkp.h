@@ -110,6 +110,9 @@ typedef struct zkp_transcript {
 /* Bind to HIP device `device` (ordinal). One ctx per caller thread. */
 int zkp_ctx_create(int device, zkp_ctx** out);
 void zkp_ctx_destroy(zkp_ctx* ctx);
+/* Free the idle stage-session context the ctx keeps for its next zkp_session_create
+ * (at most one; it holds the last session's device buffers and domain tables). */
+int zkp_ctx_trim(zkp_ctx* ctx);
 /* Last error message for ctx (static storage owned by ctx). */
 const char* zkp_last_error(const zkp_ctx* ctx);
 void zkp_free(void* p);

@@ -79,7 +79,7 @@ EXPORTED = [
     "zkp_composition_commit", "zkp_ood_frame", "zkp_deep_fri", "zkp_query", "zkp_comm_host_create",
     "zkp_session_shape",
     "zkp_channel_create", "zkp_channel_destroy", "zkp_channel_commit", "zkp_channel_commit_felts",
-    "zkp_channel_draw", "zkp_channel_seed", "zkp_channel_query_positions",
+    "zkp_channel_draw", "zkp_channel_seed", "zkp_channel_query_positions", "zkp_ctx_trim",
 ]
 
 # zkp_host_transport callbacks (include/zkp.h)
@@ -132,6 +132,7 @@ def load():
         L.zkp_ctx_create.argtypes = [i32, ctypes.POINTER(vp)]
         L.zkp_ctx_destroy.argtypes = [vp]
         L.zkp_ctx_destroy.restype = None
+        L.zkp_ctx_trim.argtypes = [vp]
         L.zkp_last_error.argtypes = [vp]
         L.zkp_last_error.restype = ctypes.c_char_p
         L.zkp_free.argtypes = [vp]
@@ -308,6 +309,10 @@ class Context:
         if cls._default is None:
             cls._default = cls(0)
         return cls._default
+
+    def trim(self):
+        """zkp_ctx_trim: free the idle stage-session context kept for the next session."""
+        self._check(self.lib.zkp_ctx_trim(self.ptr), "zkp_ctx_trim")
 
     def close(self):
         if self.ptr:

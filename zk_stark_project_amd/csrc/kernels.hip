@@ -999,6 +999,15 @@ void Prof::end(hipStream_t s) {
 
 
 
+__global__ void k_noop() {}
+
+void preload_kernels_module() {
+  hipFuncAttributes fa;
+  (void)hipFuncGetAttributes(&fa, (const void*)k_expand_powers);
+}
+
+void warm_stream(hipStream_t s) { hipLaunchKernelGGL(k_noop, dim3(1), dim3(64), 0, s); }
+
 void launch_build_levels(Prof& prof, hipStream_t s, felt* tab, uint32_t top) {
   LAUNCH(prof, "build_levels", s, (double)(1ull << top) * 32.0,
          hipLaunchKernelGGL(k_build_levels, dim3(grid_stride_blocks(1ull << top)), dim3(TPB), 0, s, tab, top));

@@ -1251,9 +1251,9 @@ static void merkle_pass(Prof& prof, hipStream_t s, const MerkleArgs& a, uint32_t
 // upper levels: wide levels by lane passes (4 levels each), the narrow top by
 // the LDS-fused kernel (9 levels per launch, parallel tail)
 bool merkle_upper(Prof& prof, hipStream_t s, uint32_t* nodes, uint64_t L, const MerkleTail* tail) {
-  // ZKP_MERKLE_LANE_MIN=k (A/B switch): lane passes down to 2^k nodes (default 18)
-  static const uint32_t lane_min_log =
-      getenv("ZKP_MERKLE_LANE_MIN") ? std::max(2, atoi(getenv("ZKP_MERKLE_LANE_MIN"))) : 18u;
+  // lane passes down to 2^18 nodes (2^10-2^16 measured slower: profiles/r03_ab_merkle_lane_min.txt,
+  // r04_ab_merkle_lane_min16.txt)
+  constexpr uint32_t lane_min_log = 18;
   while (L > 1) {
     MerkleArgs a{};
     a.nodes = nodes;
@@ -1291,7 +1291,6 @@ bool launch_merkle_lde(Prof& prof, hipStream_t s, const felt* lde, uint32_t cols
   // each lane hashes 2 rows and merges them (H = 1): measured faster than deeper
   // lane subtrees, whose extra live digests cost waves (kbench_merkle.cpp)
   const uint32_t H = L >= 2 ? 1 : 0;
-  static const bool no_preload = getenv("ZKP_NO_LEAF_PRELOAD") != nullptr;  // A/B switch
   if (gl) {  // lazy GlobalUpdate columns (wide rows: the generic lane pass)
     a.gl = *gl;
     merkle_pass<4>(prof, s, a, H, "merkle_lde", (double)L * (gl->wi * 16.0 + 64.0));
@@ -1306,7 +1305,7 @@ bool launch_merkle_lde(Prof& prof, hipStream_t s, const felt* lde, uint32_t cols
     break;
     switch (cols) { ZKP_LEAF2D(2) ZKP_LEAF2D(3) ZKP_LEAF2D(4) ZKP_LEAF2D(5) ZKP_LEAF2D(6) ZKP_LEAF2D(7) ZKP_LEAF2D(8) }
 #undef ZKP_LEAF2D
-  } else if (H == 1 && cols <= 8 && !no_preload) {
+  } else if (H == 1 && cols <= 8) {  // rows preloaded (profiles/r03_ab_leaf_preload.txt)
     const double bytes = (double)L * (cols * 16.0 + 48.0);
     const dim3 g(blocks_for(L >> 1));
 #define ZKP_LEAF2(CC) \
@@ -1330,8 +1329,7 @@ bool launch_merkle_fri(Prof& prof, hipStream_t s, const felt* E, uint64_t m16, u
   a.cols = F;
   a.nodes = nodes;
   a.L = R;
-  static const bool no_quad = getenv("ZKP_NO_QUAD_LEAVES") != nullptr;  // A/B switch
-  if (F == 16 && R <= (1ull << 12) && !no_quad) {
+  if (F == 16 && R <= (1ull << 12)) {  // profiles/r02_ab_quad_leaves.txt
     // small layers (<= 2^12 rows): one quad of lanes per row, 64 rows and 6 levels
     // per block. At 2^15 rows the quads' extra instructions made it slower
     // (72 vs 53 us); at 2^11 / 2^7 / 2^3 rows it is faster (30/22/21 vs 40/34/29 us)
@@ -1358,6 +1356,11 @@ bool launch_merkle_fri(Prof& prof, hipStream_t s, const felt* E, uint64_t m16, u
   while (H < 2 && (1ull << (H + 1)) <= R) H++;
   merkle_pass<1>(prof, s, a, H, "merkle_fri", (double)R * (F * 16.0 + 64.0));
   return merkle_upper(prof, s, nodes, R >> H, tail);
+}
+
+void preload_merkle_module() {
+  hipFuncAttributes fa;
+  (void)hipFuncGetAttributes(&fa, (const void*)k_merkle_level);
 }
 
 void launch_leaf_hash_lde(Prof& prof, hipStream_t s, const felt* lde, uint32_t cols, uint32_t logB, uint64_t n,
@@ -1513,8 +1516,7 @@ void launch_merkle_from_shards(Prof& prof, hipStream_t s, const uint32_t* recv, 
   fin.done = done;
   const MerkleTail* tail = done ? &fin : nullptr;
   const uint64_t L = 1ull << (logB + logrr);
-  static const bool separate = getenv("ZKP_LEAF_UNPACK") != nullptr;  // A/B switch: the unfused unpack pass
-  if (separate || L < 4) {
+  if (L < 4) {
     LAUNCH(prof, "leaf_unpack", s, (double)L * 64.0,
            hipLaunchKernelGGL(k_leaf_unpack, dim3(blocks_for(L)), dim3(TPB), 0, s, recv, logB, logrr, logK, nodes, L));
     merkle_upper(prof, s, nodes, L, tail);

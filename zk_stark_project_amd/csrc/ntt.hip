@@ -428,6 +428,11 @@ __global__ __launch_bounds__(NT) void k_ntt8(Ntt8Args a) {
 
 }  // namespace
 
+void preload_ntt_module() {
+  hipFuncAttributes fa;
+  (void)hipFuncGetAttributes(&fa, (const void*)k_ntt_pass);
+}
+
 std::vector<NttPass> ntt_plan(uint32_t logn, bool dit) {
   const uint32_t KMAX = 8, LOGE = 12;
   std::vector<NttPass> out;

@@ -35,6 +35,14 @@ struct Prof {
 // offsets, and the largest trace the OOD evaluation's block tree takes; entry
 // points return ZKP_ERR_TRACE_SHAPE past them
 constexpr uint32_t MAX_LOG_DOMAIN = 28, MAX_LOG_TRACE = 23;
+// Load each kernel translation unit's gfx950 code object on the current device
+// now (zkp_ctx_create) instead of at its first launch inside a proof: HIP loads
+// a fat binary's code object lazily, on the first use of one of its kernels.
+void preload_kernels_module();
+void preload_merkle_module();
+void preload_ntt_module();
+// one empty launch on `s`: HIP binds a stream to a hardware queue at its first dispatch
+void warm_stream(hipStream_t s);
 
 // ---------------------------------------------------------------- NTT
 // One LDS pass of K radix-2 stages (see kernels.hip). `dit` = bit-reversed in
