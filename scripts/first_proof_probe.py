@@ -37,6 +37,12 @@ def main():
                                  sorted(tab.items(), key=lambda kv: -kv[1]["ms"])}
     ctx.reset_stats()
     out["warm_ms"] = [once(ctx) for _ in range(3)]
+    # the same warm context after the GPU sat idle (clock ramp / power state)
+    idle = []
+    for _ in range(3):
+        time.sleep(0.5)
+        idle.append(once(ctx))
+    out["warm_after_idle_0.5s_ms"] = idle
     t0 = time.perf_counter()
     ctx2 = _native.Context(0)
     out["second_ctx_create_ms"] = (time.perf_counter() - t0) * 1e3

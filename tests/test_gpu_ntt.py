@@ -33,3 +33,12 @@ def test_field_op_edge_cases():
 def test_ntt_exact_redo_rounds():
     out = run("ntt_check")
     assert "0 mismatching" in out, out
+
+
+def test_eval_mimc_exact_redo():
+    """k_eval_mimc's exact recomputation, driven on purpose (tests/native/eval_check.cpp):
+    every output equals the host's exact arithmetic and the redo branch was taken."""
+    out = run("eval_check")
+    assert ", 0 mismatching," in out, out
+    redo = int(out.strip().splitlines()[-1].split(",")[-1].split()[0])
+    assert redo > 0, out

@@ -335,6 +335,20 @@ __device__ __forceinline__ CePoint ce_point(const EvalCommon& c, uint64_t q) {
   return p;
 }
 
+// ZKP_COUNT_REDO (tests/native/eval_check.cpp builds this file with it): count the waves
+// that take the exact recomputation, so the test knows its inputs reached it
+#ifdef ZKP_COUNT_REDO
+__device__ unsigned long long zkp_redo_waves;
+#define ZKP_REDO_TAKEN()                                                             \
+  do {                                                                               \
+    if ((threadIdx.x & 63) == 0) atomicAdd(&zkp_redo_waves, 1ull);                   \
+  } while (0)
+#else
+#define ZKP_REDO_TAKEN() \
+  do {                   \
+  } while (0)
+#endif
+
 __global__ __launch_bounds__(TPB) void k_eval_mimc(EvalCommon c, MimcEvalArgs a, const felt* __restrict__ lde,
                                                    const felt* __restrict__ dinv, felt* __restrict__ comp) {
   const uint64_t M = (uint64_t)c.cel << c.logn;
@@ -363,7 +377,10 @@ __global__ __launch_bounds__(TPB) void k_eval_mimc(EvalCommon c, MimcEvalArgs a,
     };
     Rare rq;
     felt v = point(std::true_type{}, rq);
-    if (rq.any()) v = point(std::false_type{}, rq);
+    if (rq.any()) {
+      v = point(std::false_type{}, rq);
+      ZKP_REDO_TAKEN();
+    }
     comp[q] = v;
   });
 }
@@ -906,6 +923,29 @@ __global__ __launch_bounds__(TPB) void k_gu_check(const felt* __restrict__ T, ui
   }
 }
 
+// The MiMC trace against its AIR before the proof's shortcuts are chosen: every row's
+// transition x[t+1] = (x[t] + K[t mod 64])^7 (K = get_round_constants(), helper.rs:404-406)
+// and the two assertions x[0] = v0, x[n-1] = v1. A trace that satisfies them has a
+// composition polynomial of degree < 6n, so the derived last composition column
+// (LastCol) is exact; any failure sets *bad (one store per failing wave).
+__global__ __launch_bounds__(TPB) void k_mimc_check(const felt* __restrict__ T, uint64_t n, felt v0, felt v1,
+                                                    uint32_t* __restrict__ bad) {
+  const uint64_t t = blockIdx.x * (uint64_t)TPB + threadIdx.x;
+  bool ok = true;
+  if (t < n) {
+    const felt x = T[t];
+    if (t + 1 < n) {
+      const felt u = add(x, make((t % 64 + 1) * 1000000ull, 0));
+      const felt u3 = mul(mul(u, u), u), u7 = mul(mul(u3, u3), u);
+      ok = eq(T[t + 1], u7);
+    }
+    if (t == 0) ok = ok && eq(x, v0);
+    if (t == n - 1) ok = ok && eq(x, v1);
+  }
+  const uint64_t failing = __builtin_amdgcn_ballot_w64(!ok);
+  if (failing && (threadIdx.x & 63) == (uint32_t)__builtin_ctzll(failing)) *bad = 1u;
+}
+
 // coefficient columns (bit-reversed, scaled by n) at the positions [p0, p0 + np):
 // coef_{d+i}[p] = k*(1 - w_n^-rev(p))*coef_i[p] + c_i
 __global__ __launch_bounds__(TPB) void k_gu_coef(felt* __restrict__ coef, uint32_t d, uint32_t logn, felt k,
@@ -1046,6 +1086,16 @@ static void launch_den_table(Prof& prof, hipStream_t s, const PointMap& m, uint6
          hipLaunchKernelGGL(k_den_table, dim3(blocks_for((count + EVAL_CH - 1) / EVAL_CH)), dim3(TPB), 0, s, m, count,
                             c0, c1, two, prod, table));
 }
+
+#ifdef ZKP_COUNT_REDO
+// host: the exact-pass waves of k_eval_mimc since the last call (and reset)
+unsigned long long zkp_redo_waves_take() {
+  unsigned long long v = 0, z = 0;
+  (void)hipMemcpyFromSymbol(&v, HIP_SYMBOL(zkp_redo_waves), sizeof v);
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(zkp_redo_waves), &z, sizeof z);
+  return v;
+}
+#endif
 
 void launch_eval_mimc(Prof& prof, hipStream_t s, const EvalCommon& c, const MimcEvalArgs& a, const felt* lde,
                       felt* comp) {
@@ -1239,6 +1289,11 @@ void launch_gu_check(Prof& prof, hipStream_t s, const felt* T, uint32_t d, uint3
   LAUNCH(prof, "gu_pair", s, (double)cnt * 32.0,
          hipLaunchKernelGGL(k_gu_check, dim3(blocks_for(cnt)), dim3(TPB), 0, s, T, d, logn, k, c0, cw, t0, logtn,
                             cval, bad));
+}
+
+void launch_mimc_check(Prof& prof, hipStream_t s, const felt* T, uint64_t n, felt v0, felt v1, uint32_t* bad) {
+  LAUNCH(prof, "trace_check", s, (double)n * 16.0,
+         hipLaunchKernelGGL(k_mimc_check, dim3(blocks_for(n)), dim3(TPB), 0, s, T, n, v0, v1, bad));
 }
 
 void launch_gu_coef(Prof& prof, hipStream_t s, felt* coef, uint32_t d, uint32_t logn, felt k, const felt* itwn,

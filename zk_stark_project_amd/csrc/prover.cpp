@@ -156,6 +156,18 @@ void ProofRun::trace_stage(const zkp_felt* h_trace) {
     // kernels are queued (late_pairs_upload; pair_failed joins it)
     const bool late_pairs = paired && h_trace;
     if (paired && !h_trace) grp.push_back({d, d});
+    // a device-resident paired trace is checked before its columns are transformed:
+    // a failing pair falls back to the plain interpolation of [d, w) in the group
+    // loop below, instead of a second proof (world 1; sharded proofs all-gather
+    // their flags and prove again)
+    const bool early_pairs = paired && !h_trace && R == 1;
+    if (early_pairs) {
+      launch_gu_check(pf, st, d_trace, d, logn, air.k, 0, d, 0, logn, gu_cval, gu_bad);
+      early_check_launch(gu_bad);
+    }
+    // MiMC: the trace against its transitions and assertions (k_mimc_check), read by
+    // composition_stage to choose the derived last column (LastCol)
+    const bool mimc_check = allow_shortcuts && air.id == ZKP_AIR_MIMC && w == 1;
     const bool piped = h_trace && grp.size() > 1;
     const size_t G = grp.size();
     if (piped) {  // the copy stream starts after everything already queued
@@ -180,9 +192,20 @@ void ProofRun::trace_stage(const zkp_felt* h_trace) {
       } else if (h_trace && g == 0) {
         ctx->upload(dcol, h_trace, (size_t)w * n * 16);
       }
-      if (c0 >= wd) {  // paired columns d+i, i in [c0 - d, c0 - d + cw): check, then derive
+      if (g == 0 && mimc_check) {
+        uint32_t* dflag = ctx->buf<uint32_t>("mimc_bad", 4);
+        HIP_CHECK(hipMemsetAsync(dflag, 0, 16, st));
+        launch_mimc_check(pf, st, d_trace, n, air.a_val[0], air.a_val[1], dflag);
+        early_check_launch(dflag);
+      }
+      if (c0 >= wd && early_pairs && early_check_failed()) {
+        // a pair fails its transition: these columns are interpolated and extended
+        // like the others, and nothing downstream derives them
+        paired = false;
+        gu_lazy_on = false;
+      } else if (c0 >= wd) {  // paired columns d+i, i in [c0 - d, c0 - d + cw): check, then derive
         const uint32_t i0 = c0 - d;
-        launch_gu_check(pf, st, d_trace, d, logn, air.k, i0, cw, 0, logn, gu_cval, gu_bad);
+        if (!early_pairs) launch_gu_check(pf, st, d_trace, d, logn, air.k, i0, cw, 0, logn, gu_cval, gu_bad);
         launch_gu_coef(pf, st, coef, d, logn, air.k, ctx->itws(logN) + ((n >> 1) - 1), i0, cw, 0, n, gu_cval);
         if (!gu_lazy_on) launch_gu_lde(pf, st, tlde, d, logn, logBl, air.k, i0, cw, gu_cval, l0_table());
         continue;
@@ -265,7 +288,10 @@ void ProofRun::composition_stage() {
     // the last composition column derived in the leaf pass (LastCol): the rank's
     // LDE cosets are exactly its CE cosets, whose evaluations stay in `comp`
     static const bool no_derive = getenv("ZKP_NO_DERIVE_LAST") != nullptr;  // A/B switch
-    const bool derive = allow_shortcuts && !no_derive && logce == logB && C >= 2 && C <= 8 && cel == Bl && u0 == j0;
+    // a trace that fails k_mimc_check proves without it (its dropped segments would
+    // not be zero); one that passes cannot raise lc_bad, which stays as the backstop
+    const bool derive = allow_shortcuts && !no_derive && logce == logB && C >= 2 && C <= 8 && cel == Bl && u0 == j0 &&
+                        !(pre_checked && early_check_failed());
     derive_last = derive;
     if (derive) {
       lc_bad = ctx->buf<uint32_t>("lc_bad", 4);
@@ -739,6 +765,21 @@ void ProofRun::late_pairs_upload() {
   gu_late_check = true;
 }
 
+// the early trace check: its flag word to the host behind the check kernel, and the event
+void ProofRun::early_check_launch(uint32_t* dflag) {
+  HIP_CHECK(hipMemcpyAsync(ctx->host_flag(), dflag, 4, hipMemcpyDeviceToHost, st));
+  HIP_CHECK(hipEventRecord(ctx->ev_check, st));
+  pre_checked = true;
+}
+
+// the early check's flag (waits for the check kernel only: everything queued after it
+// keeps the GPU busy meanwhile)
+bool ProofRun::early_check_failed() {
+  if (!pre_checked) return false;
+  HIP_CHECK(hipEventSynchronize(ctx->ev_check));
+  return *ctx->host_flag() != 0;
+}
+
 // a paired trace whose transitions did not hold (one 4-byte read after the proof's last kernels)
 bool ProofRun::pair_failed() {
   if (!paired) return false;
@@ -813,7 +854,8 @@ zkp_ctx* new_ctx(int device) {
       hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&c->copy, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess) {
+      hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_check, hipEventDisableTiming) != hipSuccess) {
     delete c;
     return nullptr;
   }

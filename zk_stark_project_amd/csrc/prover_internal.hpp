@@ -54,6 +54,15 @@ struct zkp_ctx {
   // of the main stream's coset LDEs (ordered in with events)
   hipStream_t copy = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  // a proof's early trace check (MiMC transitions, GlobalUpdate pairs): its flag is
+  // copied to flag_h (pinned) and ev_check recorded, so a later stage reads it
+  // without stalling the queue (the GPU passed it long before)
+  hipEvent_t ev_check = nullptr;
+  uint32_t* flag_h = nullptr;
+  uint32_t* host_flag() {
+    if (!flag_h) HIP_CHECK(hipHostMalloc((void**)&flag_h, 64, hipHostMallocDefault));
+    return flag_h;
+  }
   Prof prof;
   std::string err;
   std::map<std::string, DevBuf> bufs;
@@ -305,6 +314,8 @@ struct zkp_ctx {
     for (auto e : prof.pool) (void)hipEventDestroy(e);
     for (auto e : up_ev) (void)hipEventDestroy(e);
     if (ev_fork) (void)hipEventDestroy(ev_fork);
+    if (ev_check) (void)hipEventDestroy(ev_check);
+    if (flag_h) (void)hipHostFree(flag_h);
     if (ev_join) (void)hipEventDestroy(ev_join);
     if (copy) (void)hipStreamDestroy(copy);
     if (side) (void)hipStreamDestroy(side);
@@ -506,6 +517,10 @@ struct ProofRun {
   uint32_t* lc_bad = nullptr;    // this rank's flag (4 words)
   uint32_t* lc_flags = nullptr;  // sharded: every rank's flags (all-gathered)
   bool lastcol_failed();
+  // the early trace check (trace_stage -> composition_stage / the paired group)
+  bool pre_checked = false;
+  void early_check_launch(uint32_t* dflag);
+  bool early_check_failed();
   bool h_partial = false;  // a host trace of which only this rank's columns were uploaded
   // stage sessions (zkp_session_*): the caller's channel draws every coefficient, so
   // commitments return their roots to the host and no device transcript runs

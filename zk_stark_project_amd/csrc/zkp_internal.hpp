@@ -279,6 +279,8 @@ void launch_eval_linear_pts(Prof& prof, hipStream_t s, const EvalCommon& c, cons
 // coefficient columns at positions [p0, p0 + np) (itwn = the inverse w_n table
 // level); lde: the derived LDE columns over Bl cosets (l0 = L_0 over those cosets,
 // launch_l0_table)
+// MiMC trace vs its transition and assertions (sets *bad on any failing row)
+void launch_mimc_check(Prof& prof, hipStream_t s, const felt* T, uint64_t n, felt v0, felt v1, uint32_t* bad);
 void launch_gu_check(Prof& prof, hipStream_t s, const felt* T, uint32_t d, uint32_t logn, felt k, uint32_t c0,
                      uint32_t cw, uint64_t t0, uint32_t logtn, felt* cval, uint32_t* bad);
 void launch_gu_coef(Prof& prof, hipStream_t s, felt* coef, uint32_t d, uint32_t logn, felt k, const felt* itwn,
