@@ -76,5 +76,33 @@ int main(int argc, char** argv) {
       printf("L=2^%-2d tail=%-12s %8.2f us per tree top\n", __builtin_ctzll(L), opn[op], ms * 1e3 / reps);
     }
   }
+  // FRI layer commitments (leaf hashing of 16-felt rows + the tree + the coin step) by
+  // the rows' size and the quad-leaf threshold
+  extern uint32_t fri_quad_max_log;
+  felt* E;
+  const uint64_t Rmax = 1ull << 16;
+  CK(hipMalloc(&E, Rmax * 16 * 16));
+  CK(hipMemset(E, 0x11, Rmax * 16 * 16));
+  for (uint32_t logR : {11u, 13u, 15u}) {
+    for (uint32_t qmax : {12u, 13u, 15u}) {
+      fri_quad_max_log = qmax;
+      MerkleTail t{};
+      t.done = done;
+      t.coin_seed = seed;
+      t.alpha_out = alpha;
+      t.root_out = root_out;
+      t.op = MERKLE_TAIL_FRI_COIN;
+      const uint64_t m16 = (1ull << logR) >> 3;  // B = 8 cosets
+      for (int i = 0; i < 5; i++) launch_merkle_fri(pf, st, E, m16, 3, 16, nodes, &t);
+      CK(hipStreamSynchronize(st));
+      CK(hipEventRecord(e0, st));
+      for (int i = 0; i < reps; i++) launch_merkle_fri(pf, st, E, m16, 3, 16, nodes, &t);
+      CK(hipEventRecord(e1, st));
+      CK(hipEventSynchronize(e1));
+      float ms = 0;
+      CK(hipEventElapsedTime(&ms, e0, e1));
+      printf("FRI layer 2^%-2u rows quad_max=2^%-2u %8.2f us per commitment\n", logR, qmax, ms * 1e3 / reps);
+    }
+  }
   return 0;
 }

@@ -26,7 +26,7 @@ __device__ __forceinline__ uint32_t sel4(uint32_t q, uint32_t x0, uint32_t x1, u
 // One BLAKE3 compression (chunk counter 0, 64-byte block) by a quad: lane q
 // holds chaining-value words q (a) and 4+q (b) in and out.
 __device__ __forceinline__ void compress_quad(const uint32_t m[16], uint32_t q, uint32_t flags, uint32_t& a,
-                                              uint32_t& b) {
+                                              uint32_t& b, uint32_t blen = 64) {
   constexpr uint8_t S[7][16] = {{0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15},
                                 {2, 6, 3, 10, 7, 0, 4, 13, 1, 11, 12, 5, 9, 14, 15, 8},
                                 {3, 4, 10, 12, 13, 2, 7, 14, 6, 5, 9, 0, 11, 15, 8, 1},
@@ -35,7 +35,7 @@ __device__ __forceinline__ void compress_quad(const uint32_t m[16], uint32_t q, 
                                 {9, 14, 11, 5, 8, 12, 15, 1, 13, 3, 0, 10, 2, 6, 4, 7},
                                 {11, 15, 5, 0, 1, 9, 8, 6, 14, 10, 2, 12, 3, 4, 7, 13}};
   uint32_t c = sel4(q, b3::iv(0), b3::iv(1), b3::iv(2), b3::iv(3));  // v[8..12) = IV[0..4)
-  uint32_t d = sel4(q, 0u, 0u, 64u, flags);                          // counter, block_len, flags
+  uint32_t d = sel4(q, 0u, 0u, blen, flags);                         // counter, block_len, flags
 #define B3Q_G(x, y)                 \
   a = a + b + (x);                  \
   d = b3::rotr(d ^ a, 16);          \
@@ -115,6 +115,69 @@ __device__ __forceinline__ void quad_gather8(uint32_t a, uint32_t b, uint32_t ou
   out[5] = (uint32_t)__builtin_amdgcn_mov_dpp((int)b, 0x55, 0xF, 0xF, false);
   out[6] = (uint32_t)__builtin_amdgcn_mov_dpp((int)b, 0xAA, 0xF, 0xF, false);
   out[7] = (uint32_t)__builtin_amdgcn_mov_dpp((int)b, 0xFF, 0xF, 0xF, false);
+}
+
+// ---- the device coin and small hashes by a quad (lanes q = 0..3 of one quad, all
+// active): the serial transcript steps between the proof's stages, at ~1/4 of one
+// lane's compression latency. Lane q holds words q and 4+q of every 8-word value.
+
+// Blake3_256::hash_elements of nf <= 64 felts (one chunk), get(i) read by every lane
+template <typename Get>
+__device__ __forceinline__ void quad_hash_felts(Get get, uint32_t nf, uint32_t q, uint32_t& o0, uint32_t& o1) {
+  o0 = sel4(q, b3::iv(0), b3::iv(1), b3::iv(2), b3::iv(3));
+  o1 = sel4(q, b3::iv(4), b3::iv(5), b3::iv(6), b3::iv(7));
+  const uint32_t nblk = nf ? (nf + 3) / 4 : 1;
+  for (uint32_t blk = 0; blk < nblk; blk++) {
+    uint32_t m[16];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const uint32_t i = 4 * blk + k;
+      const felt v = i < nf ? get(i) : fp::zero();
+      m[4 * k + 0] = (uint32_t)v.lo;
+      m[4 * k + 1] = (uint32_t)(v.lo >> 32);
+      m[4 * k + 2] = (uint32_t)v.hi;
+      m[4 * k + 3] = (uint32_t)(v.hi >> 32);
+    }
+    const uint32_t cnt = nf - 4 * blk < 4 ? nf - 4 * blk : 4;
+    const uint32_t fl = (blk == 0 ? b3::CHUNK_START : 0u) | (blk + 1 == nblk ? (b3::CHUNK_END | b3::ROOT) : 0u);
+    compress_quad(m, q, fl, o0, o1, nf ? 16 * cnt : 0u);
+  }
+}
+
+// reseed: seed <- BLAKE3(seed || d), d given whole (8 words) to every lane
+__device__ __forceinline__ void qcoin_reseed(uint32_t q, uint32_t& s0, uint32_t& s1, const uint32_t d[8]) {
+  uint32_t m[16];
+  quad_gather8(s0, s1, m);
+#pragma unroll
+  for (int i = 0; i < 8; i++) m[8 + i] = d[i];
+  s0 = sel4(q, b3::iv(0), b3::iv(1), b3::iv(2), b3::iv(3));
+  s1 = sel4(q, b3::iv(4), b3::iv(5), b3::iv(6), b3::iv(7));
+  compress_quad(m, q, b3::CHUNK_START | b3::CHUNK_END | b3::ROOT, s0, s1);
+}
+
+// draw candidate ctr: the first 16 bytes of BLAKE3(seed || ctr_le64), in every lane
+__device__ __forceinline__ felt qcoin_candidate(uint32_t q, uint32_t s0, uint32_t s1, uint64_t ctr) {
+  uint32_t m[16];
+  quad_gather8(s0, s1, m);
+  m[8] = (uint32_t)ctr;
+  m[9] = (uint32_t)(ctr >> 32);
+#pragma unroll
+  for (int i = 10; i < 16; i++) m[i] = 0;
+  uint32_t o0 = sel4(q, b3::iv(0), b3::iv(1), b3::iv(2), b3::iv(3));
+  uint32_t o1 = sel4(q, b3::iv(4), b3::iv(5), b3::iv(6), b3::iv(7));
+  compress_quad(m, q, b3::CHUNK_START | b3::CHUNK_END | b3::ROOT, o0, o1, 40);
+  uint32_t g[8];
+  quad_gather8(o0, o1, g);
+  return fp::make((uint64_t)g[0] | ((uint64_t)g[1] << 32), (uint64_t)g[2] | ((uint64_t)g[3] << 32));
+}
+
+// DefaultRandomCoin::draw: the first candidate < p (counter advanced), in every lane
+__device__ __forceinline__ felt qcoin_draw(uint32_t q, uint32_t s0, uint32_t s1, uint64_t* ctr) {
+  for (int i = 0; i < 1000; i++) {
+    const felt v = qcoin_candidate(q, s0, s1, ++*ctr);
+    if (!fp::ge_p(v)) return v;
+  }
+  return fp::zero();
 }
 
 }  // namespace

@@ -165,7 +165,7 @@ __device__ __forceinline__ void fri_leaf_quad(const MerkleArgs& a, uint64_t i, u
       m[4 * k + 3] = (uint32_t)(v.hi >> 32);
     }
     const uint32_t fl = (blk == 0 ? b3::CHUNK_START : 0u) | (blk == 3 ? (b3::CHUNK_END | b3::ROOT) : 0u);
-    compress_quad_r(m, q, fl, o0, o1);
+    compress_quad(m, q, fl, o0, o1);
   }
 }
 
@@ -218,7 +218,7 @@ __global__ __launch_bounds__(256) void k_merkle_fused(MerkleArgs a) {
         store_digest(a.nodes + (L + base + 2 * t) * 8, d0);
         store_digest(a.nodes + (L + base + 2 * t + 1) * 8, d1);
       }
-      merge8<true>(d0, d1, m);
+      merge8<false>(d0, d1, m);
       store_digest(a.nodes + ((L >> 1) + (base >> 1) + t) * 8, m);
 #pragma unroll
       for (int i = 0; i < 8; i++) sd[t * 9 + i] = m[i];
@@ -236,7 +236,7 @@ __global__ __launch_bounds__(256) void k_merkle_fused(MerkleArgs a) {
         uint32_t mm[16];
 #pragma unroll
         for (int i = 0; i < 8; i++) { mm[i] = sd[(2 * nd) * 9 + i]; mm[8 + i] = sd[(2 * nd + 1) * 9 + i]; }
-        merge_quad<true>(mm, q, o0, o1);
+        merge_quad<false>(mm, q, o0, o1);
       }
       lvl >>= 1;
       lbase >>= 1;
@@ -255,7 +255,7 @@ __global__ __launch_bounds__(256) void k_merkle_fused(MerkleArgs a) {
       uint32_t l[8], r[8];
 #pragma unroll
       for (int i = 0; i < 8; i++) { l[i] = sd[(2 * t) * 9 + i]; r[i] = sd[(2 * t + 1) * 9 + i]; }
-      merge8<true>(l, r, o);
+      merge8<false>(l, r, o);
     }
     lvl >>= 1;
     lbase >>= 1;
@@ -286,7 +286,7 @@ __global__ __launch_bounds__(256) void k_merkle_fused(MerkleArgs a) {
         const uint32_t* src = a.nodes + (uint64_t)(G + 2 * nd) * 8;  // the node's two children, adjacent
 #pragma unroll
         for (int k = 0; k < 16; k++) mm[k] = src[k];
-        merge_quad<true>(mm, q, o0, o1);
+        merge_quad<false>(mm, q, o0, o1);
         sd[nd * 9 + q] = o0;
         sd[nd * 9 + 4 + q] = o1;
         uint32_t* dst = a.nodes + (uint64_t)(G / 2 + nd) * 8;
@@ -298,7 +298,7 @@ __global__ __launch_bounds__(256) void k_merkle_fused(MerkleArgs a) {
         uint32_t l[8], r[8], o[8];
         load_digest(a.nodes + (uint64_t)(G + 2 * i) * 8, l);
         load_digest(a.nodes + (uint64_t)(G + 2 * i + 1) * 8, r);
-        merge8<true>(l, r, o);
+        merge8<false>(l, r, o);
         store_digest(a.nodes + (uint64_t)(G / 2 + i) * 8, o);
 #pragma unroll
         for (int k = 0; k < 8; k++) sd[i * 9 + k] = o[k];
@@ -313,7 +313,7 @@ __global__ __launch_bounds__(256) void k_merkle_fused(MerkleArgs a) {
           uint32_t mm[16];
 #pragma unroll
           for (int k = 0; k < 8; k++) { mm[k] = sd[(2 * nd) * 9 + k]; mm[8 + k] = sd[(2 * nd + 1) * 9 + k]; }
-          merge_quad<true>(mm, q, o0, o1);
+          merge_quad<false>(mm, q, o0, o1);
         }
         __syncthreads();
         if (t < 4 * sl) {
@@ -330,7 +330,7 @@ __global__ __launch_bounds__(256) void k_merkle_fused(MerkleArgs a) {
         uint32_t l[8], r[8];
 #pragma unroll
         for (int k = 0; k < 8; k++) { l[k] = sd[(2 * t) * 9 + k]; r[k] = sd[(2 * t + 1) * 9 + k]; }
-        merge8<true>(l, r, o);
+        merge8<false>(l, r, o);
       }
       __syncthreads();
       if (t < sl) {
@@ -518,12 +518,12 @@ __device__ __forceinline__ felt dcoin_draw(const uint32_t s[8], uint64_t* ctr) {
 // on a rejection), Algebraic = powers of one draw, Horner = the powers reversed
 __device__ __forceinline__ void dcoin_draw_coeffs_block(const uint32_t s[8], uint32_t method, uint32_t ncoef, felt* out,
                                         felt* s_alpha, int* s_rej) {
-  if (threadIdx.x == 0) {
-    *s_rej = 0;
-    if (method != ZKP_BATCHING_LINEAR) {
-      uint64_t ctr = 0;
-      *s_alpha = dcoin_draw(s, &ctr);
-    }
+  if (threadIdx.x == 0) *s_rej = 0;
+  if (method != ZKP_BATCHING_LINEAR && threadIdx.x < 4) {  // one draw, by the first quad
+    const uint32_t q = threadIdx.x;
+    uint64_t ctr = 0;
+    const felt a = qcoin_draw(q, s[q], s[4 + q], &ctr);
+    if (q == 0) *s_alpha = a;
   }
   __syncthreads();
   if (method == ZKP_BATCHING_LINEAR) {
@@ -598,6 +598,41 @@ __device__ __forceinline__ void hash_felts_block(Get get, uint32_t nf, uint32_t 
   __syncthreads();
 }
 
+// hash_elements for the transcript: one chunk (<= 64 felts) by the block's first
+// quad (quad_hash_felts), longer inputs by hash_felts_block; out[] in every thread
+template <typename Get>
+__device__ __forceinline__ void hash_felts_fast(Get get, uint32_t nf, uint32_t out[8], uint32_t (*s_cv)[8]) {
+  if (nf > 64) {
+    hash_felts_block(get, nf, out, s_cv);
+    if (threadIdx.x == 0)
+      for (int i = 0; i < 8; i++) s_cv[0][i] = out[i];
+  } else if (threadIdx.x < 4) {
+    const uint32_t q = threadIdx.x;
+    uint32_t o0, o1;
+    quad_hash_felts(get, nf, q, o0, o1);
+    s_cv[0][q] = o0;
+    s_cv[0][4 + q] = o1;
+  }
+  __syncthreads();
+  for (int i = 0; i < 8; i++) out[i] = s_cv[0][i];
+  __syncthreads();
+}
+
+// the block's first quad: seed <- BLAKE3(src || d) into dst (and dst2 when given)
+__device__ __forceinline__ void quad_reseed_to(const uint32_t* src, const uint32_t d[8], uint32_t* dst,
+                                               uint32_t* dst2 = nullptr) {
+  if (threadIdx.x >= 4) return;
+  const uint32_t q = threadIdx.x;
+  uint32_t s0 = src[q], s1 = src[4 + q];
+  qcoin_reseed(q, s0, s1, d);
+  dst[q] = s0;
+  dst[4 + q] = s1;
+  if (dst2) {
+    dst2[q] = s0;
+    dst2[4 + q] = s1;
+  }
+}
+
 // OOD frame -> transcript -> DEEP coefficients, on the device: reseed with
 // H(T(z) || T(zg)) and H(H_j(z)), draw the w + C DEEP coefficients, and the
 // constants kz = sum gamma_i T_i(z) + sum gamma_j H_j(z), kzg = sum gamma_i T_i(zg).
@@ -612,21 +647,11 @@ __global__ __launch_bounds__(64) void k_dt_deep_coeffs(uint32_t* __restrict__ se
   __shared__ int s_rej;
   __shared__ felt red0[64], red1[64];
   uint32_t h[8];
-  hash_felts_block([&](uint32_t i) { return i < w ? ood[2 * i] : ood[2 * (i - w) + 1]; }, 2 * w, h, s_cv);
-  if (threadIdx.x == 0) {
-    uint32_t t[8];
-    for (int i = 0; i < 8; i++) t[i] = seed[i];
-    dcoin_reseed(t, h);
-    for (int i = 0; i < 8; i++) s[i] = t[i];
-  }
+  hash_felts_fast([&](uint32_t i) { return i < w ? ood[2 * i] : ood[2 * (i - w) + 1]; }, 2 * w, h, s_cv);
+  quad_reseed_to(seed, h, s);
   __syncthreads();
-  hash_felts_block([&](uint32_t i) { return ood[2 * (w + i)]; }, C, h, s_cv);
-  if (threadIdx.x == 0) {
-    uint32_t t[8];
-    for (int i = 0; i < 8; i++) t[i] = s[i];
-    dcoin_reseed(t, h);
-    for (int i = 0; i < 8; i++) { s[i] = t[i]; seed[i] = t[i]; }
-  }
+  hash_felts_fast([&](uint32_t i) { return ood[2 * (w + i)]; }, C, h, s_cv);
+  quad_reseed_to(s, h, s, seed);
   __syncthreads();
   uint32_t t[8];
   for (int i = 0; i < 8; i++) t[i] = s[i];
@@ -661,11 +686,10 @@ __device__ __forceinline__ void dt_draw_coeffs_block(uint32_t* __restrict__ seed
   __shared__ uint32_t s[8];
   __shared__ felt s_alpha;
   __shared__ int s_rej;
-  if (threadIdx.x == 0) {
-    uint32_t t[8], d[8];
-    for (int i = 0; i < 8; i++) { t[i] = seed[i]; d[i] = root[i]; }
-    dcoin_reseed(t, d);
-    for (int i = 0; i < 8; i++) { s[i] = t[i]; seed[i] = t[i]; }
+  {
+    uint32_t d[8];
+    for (int i = 0; i < 8; i++) d[i] = root[i];
+    quad_reseed_to(seed, d, s, seed);
   }
   __syncthreads();
   uint32_t t[8];
@@ -683,16 +707,20 @@ __global__ __launch_bounds__(TPB) void k_dt_draw_coeffs(uint32_t* __restrict__ s
 __device__ __forceinline__ void dt_draw_z_block(uint32_t* __restrict__ seed, const uint32_t* __restrict__ root, felt wn, uint32_t logn,
                                 felt* __restrict__ zz, felt* __restrict__ pw) {
   __shared__ felt s_z;
-  if (threadIdx.x == 0) {
-    uint32_t t[8], d[8];
-    for (int i = 0; i < 8; i++) { t[i] = seed[i]; d[i] = root[i]; }
-    dcoin_reseed(t, d);
-    for (int i = 0; i < 8; i++) seed[i] = t[i];
+  if (threadIdx.x < 4) {  // the first quad: reseed with the root, draw z
+    const uint32_t q = threadIdx.x;
+    uint32_t s0 = seed[q], s1 = seed[4 + q], d[8];
+    for (int i = 0; i < 8; i++) d[i] = root[i];
+    qcoin_reseed(q, s0, s1, d);
+    seed[q] = s0;
+    seed[4 + q] = s1;
     uint64_t ctr = 0;
-    const felt z = dcoin_draw(t, &ctr);
-    zz[0] = z;
-    zz[1] = mul(z, wn);
-    s_z = z;
+    const felt z = qcoin_draw(q, s0, s1, &ctr);
+    if (q == 0) {
+      zz[0] = z;
+      zz[1] = mul(z, wn);
+      s_z = z;
+    }
   }
   __syncthreads();
   if (threadIdx.x >= 2) return;
@@ -716,11 +744,7 @@ __device__ __forceinline__ void coin_fri_step(uint32_t* __restrict__ seed, const
 // of the block call it; root = nodes + 8, written by this block)
 __device__ __forceinline__ void merkle_tail_op(const MerkleTail& tl, const uint32_t* root) {
   if (tl.op == MERKLE_TAIL_FRI_COIN) {
-    if (threadIdx.x == 0) {
-      uint32_t r[8];
-      load_digest(root, r);
-      coin_fri_step(tl.coin_seed, r, tl.alpha_out, tl.root_out);
-    }
+    coin_fri_step(tl.coin_seed, root, tl.alpha_out, tl.root_out);  // threads 0..3
   } else if (tl.op == MERKLE_TAIL_DRAW_COEFFS) {
     dt_draw_coeffs_block(tl.coin_seed, root, tl.method, tl.ncoef, tl.out);
   } else if (tl.op == MERKLE_TAIL_DRAW_Z) {
@@ -728,34 +752,29 @@ __device__ __forceinline__ void merkle_tail_op(const MerkleTail& tl, const uint3
   }
 }
 
-// FRI commit-loop Fiat-Shamir step (one thread): seed <- BLAKE3(seed || root),
-// alpha = first draw < p; root copied to root_out
+// FRI commit-loop Fiat-Shamir step by the block's first quad (threads 0..3): seed <-
+// BLAKE3(seed || root), alpha = first draw < p; root copied to root_out
 __device__ __forceinline__ void coin_fri_step(uint32_t* __restrict__ seed, const uint32_t* root, felt* __restrict__ alpha_out,
                               uint32_t* __restrict__ root_out) {
-  uint32_t m[16], s[8];
-  for (int i = 0; i < 8; i++) { m[i] = seed[i]; m[8 + i] = root[i]; root_out[i] = root[i]; }
-  b3::set_iv(s);
-  b3::compress_r(s, m, 0, 64, b3::CHUNK_START | b3::CHUNK_END | b3::ROOT);
-  felt a = fp::zero();
-  for (uint32_t ctr = 1; ctr <= 1000; ctr++) {
-    for (int i = 0; i < 8; i++) m[i] = s[i];
-    m[8] = ctr;
-    m[9] = 0;
-    for (int i = 10; i < 16; i++) m[i] = 0;
-    uint32_t o[8];
-    b3::set_iv(o);
-    b3::compress_r(o, m, 0, 40, b3::CHUNK_START | b3::CHUNK_END | b3::ROOT);
-    felt v = fp::make((uint64_t)o[0] | ((uint64_t)o[1] << 32), (uint64_t)o[2] | ((uint64_t)o[3] << 32));
-    if (!fp::ge_p(v)) { a = v; break; }
-  }
-  *alpha_out = a;
-  for (int i = 0; i < 8; i++) seed[i] = s[i];
+  if (threadIdx.x >= 4) return;
+  const uint32_t q = threadIdx.x;
+  uint32_t r[8];
+  for (int i = 0; i < 8; i++) r[i] = root[i];
+  uint32_t s0 = seed[q], s1 = seed[4 + q];
+  qcoin_reseed(q, s0, s1, r);
+  uint64_t ctr = 0;
+  const felt a = qcoin_draw(q, s0, s1, &ctr);
+  if (q == 0) *alpha_out = a;
+  seed[q] = s0;
+  seed[4 + q] = s1;
+  root_out[q] = r[q];
+  root_out[4 + q] = r[4 + q];
 }
 
 __global__ void k_coin_fri_layer(uint32_t* __restrict__ seed, const uint32_t* __restrict__ root,
                                  felt* __restrict__ alpha_out, uint32_t* __restrict__ root_out) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
-  coin_fri_step(seed, root, alpha_out, root_out);
+  if (blockIdx.x != 0) return;
+  coin_fri_step(seed, root, alpha_out, root_out);  // threads 0..3
 }
 
 struct SeedArg {
@@ -818,13 +837,9 @@ __global__ __launch_bounds__(TPB) void k_fri_remainder(const felt* __restrict__ 
   remainder_coeffs_block(E, logB, m, ncoef, off_inv, wd_inv, d_inv, s_c, s_tw);
   for (uint32_t k = threadIdx.x; k < ncoef; k += TPB) rem_out[k] = s_c[k];
   uint32_t h[8];
-  hash_felts_block([&](uint32_t i) { return s_c[i]; }, ncoef, h, s_cv);
-  if (threadIdx.x == 0) {
-    uint32_t t[8];
-    for (int i = 0; i < 8; i++) t[i] = seed[i];
-    dcoin_reseed(t, h);
-    for (int i = 0; i < 8; i++) { seed[i] = t[i]; commit_out[i] = h[i]; }
-  }
+  hash_felts_fast([&](uint32_t i) { return s_c[i]; }, ncoef, h, s_cv);
+  quad_reseed_to(seed, h, seed);
+  if (threadIdx.x < 8) commit_out[threadIdx.x] = h[threadIdx.x];
 }
 
 // Minimum nonce in [base, base + count) whose BLAKE3(seed || nonce) has >= bits
@@ -1188,7 +1203,7 @@ __global__ __launch_bounds__(512) void k_fri_tail(FriTailArgs a) {
         uint32_t mm[16];
 #pragma unroll
         for (int i = 0; i < 8; i++) { mm[i] = sd[(2 * nd) * 9 + i]; mm[8 + i] = sd[(2 * nd + 1) * 9 + i]; }
-        merge_quad<true>(mm, q, o0, o1);
+        merge_quad<false>(mm, q, o0, o1);
       }
       __syncthreads();
       if (nd < s) {
@@ -1200,7 +1215,7 @@ __global__ __launch_bounds__(512) void k_fri_tail(FriTailArgs a) {
       }
     }
     __syncthreads();
-    if (t == 0) {
+    if (t < 4) {
       uint32_t r[8];
 #pragma unroll
       for (int i = 0; i < 8; i++) r[i] = sd[i];  // the root (node 1)
@@ -1222,13 +1237,9 @@ __global__ __launch_bounds__(512) void k_fri_tail(FriTailArgs a) {
   remainder_coeffs_block(a.rem_E, a.logB, m, m, a.rem_off_inv, a.wd_inv, a.d_inv, s_c, s_tw);
   for (uint32_t k = t; k < m; k += blockDim.x) a.rem_out[k] = s_c[k];
   uint32_t h[8];
-  hash_felts_block([&](uint32_t i) { return s_c[i]; }, m, h, s_cv);
-  if (t == 0) {
-    uint32_t st[8];
-    for (int i = 0; i < 8; i++) st[i] = a.coin_seed[i];
-    dcoin_reseed(st, h);
-    for (int i = 0; i < 8; i++) { a.coin_seed[i] = st[i]; a.commit_out[i] = h[i]; }
-  }
+  hash_felts_fast([&](uint32_t i) { return s_c[i]; }, m, h, s_cv);
+  quad_reseed_to(a.coin_seed, h, a.coin_seed);
+  if (t < 8) a.commit_out[t] = h[t];
 }
 
 }  // namespace
@@ -1319,6 +1330,9 @@ bool launch_merkle_lde(Prof& prof, hipStream_t s, const felt* lde, uint32_t cols
   return merkle_upper(prof, s, nodes, L >> H, tail);
 }
 
+// largest FRI layer (log2 rows) whose leaves are hashed by quads (tests/native/kbench_top.cpp tunes it)
+uint32_t fri_quad_max_log = 13;
+
 bool launch_merkle_fri(Prof& prof, hipStream_t s, const felt* E, uint64_t m16, uint32_t logB, uint32_t F,
                        uint32_t* nodes, const MerkleTail* tail) {
   const uint64_t R = m16 << logB;
@@ -1329,7 +1343,7 @@ bool launch_merkle_fri(Prof& prof, hipStream_t s, const felt* E, uint64_t m16, u
   a.cols = F;
   a.nodes = nodes;
   a.L = R;
-  if (F == 16 && R <= (1ull << 12)) {  // profiles/r02_ab_quad_leaves.txt
+  if (F == 16 && R <= (1ull << fri_quad_max_log)) {  // profiles/r02_ab_quad_leaves.txt
     // small layers (<= 2^12 rows): one quad of lanes per row, 64 rows and 6 levels
     // per block. At 2^15 rows the quads' extra instructions made it slower
     // (72 vs 53 us); at 2^11 / 2^7 / 2^3 rows it is faster (30/22/21 vs 40/34/29 us)
@@ -1550,7 +1564,7 @@ __global__ __launch_bounds__(256) void k_shard_top(const uint32_t* __restrict__ 
       uint32_t l[8], r[8], o[8];
       load_digest(top + (2 * (h + t)) * 8, l);
       load_digest(top + (2 * (h + t) + 1) * 8, r);
-      merge8<true>(l, r, o);
+      merge8<false>(l, r, o);
       store_digest(top + (h + t) * 8, o);
     }
   }

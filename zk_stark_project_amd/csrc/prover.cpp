@@ -160,10 +160,13 @@ void ProofRun::trace_stage(const zkp_felt* h_trace) {
     // a failing pair falls back to the plain interpolation of [d, w) in the group
     // loop below, instead of a second proof (world 1; sharded proofs all-gather
     // their flags and prove again)
+    // (the checks run on the side stream, beside the first columns' transforms)
     const bool early_pairs = paired && !h_trace && R == 1;
     if (early_pairs) {
-      launch_gu_check(pf, st, d_trace, d, logn, air.k, 0, d, 0, logn, gu_cval, gu_bad);
-      early_check_launch(gu_bad);
+      HIP_CHECK(hipEventRecord(ctx->ev_fork, st));
+      HIP_CHECK(hipStreamWaitEvent(ctx->side, ctx->ev_fork, 0));
+      launch_gu_check(pf, ctx->side, d_trace, d, logn, air.k, 0, d, 0, logn, gu_cval, gu_bad);
+      early_check_launch(gu_bad, ctx->side);
     }
     // MiMC: the trace against its transitions and assertions (k_mimc_check), read by
     // composition_stage to choose the derived last column (LastCol)
@@ -194,10 +197,13 @@ void ProofRun::trace_stage(const zkp_felt* h_trace) {
       }
       if (g == 0 && mimc_check) {
         uint32_t* dflag = ctx->buf<uint32_t>("mimc_bad", 4);
-        HIP_CHECK(hipMemsetAsync(dflag, 0, 16, st));
-        launch_mimc_check(pf, st, d_trace, n, air.a_val[0], air.a_val[1], dflag);
-        early_check_launch(dflag);
+        HIP_CHECK(hipEventRecord(ctx->ev_fork, st));  // the trace is on the device
+        HIP_CHECK(hipStreamWaitEvent(ctx->side, ctx->ev_fork, 0));
+        HIP_CHECK(hipMemsetAsync(dflag, 0, 16, ctx->side));
+        launch_mimc_check(pf, ctx->side, d_trace, n, air.a_val[0], air.a_val[1], dflag);
+        early_check_launch(dflag, ctx->side);
       }
+      if (c0 >= wd && early_pairs) HIP_CHECK(hipStreamWaitEvent(st, ctx->ev_check, 0));  // gu_cval
       if (c0 >= wd && early_pairs && early_check_failed()) {
         // a pair fails its transition: these columns are interpolated and extended
         // like the others, and nothing downstream derives them
@@ -766,9 +772,9 @@ void ProofRun::late_pairs_upload() {
 }
 
 // the early trace check: its flag word to the host behind the check kernel, and the event
-void ProofRun::early_check_launch(uint32_t* dflag) {
-  HIP_CHECK(hipMemcpyAsync(ctx->host_flag(), dflag, 4, hipMemcpyDeviceToHost, st));
-  HIP_CHECK(hipEventRecord(ctx->ev_check, st));
+void ProofRun::early_check_launch(uint32_t* dflag, hipStream_t s) {
+  HIP_CHECK(hipMemcpyAsync(ctx->host_flag(), dflag, 4, hipMemcpyDeviceToHost, s));
+  HIP_CHECK(hipEventRecord(ctx->ev_check, s));
   pre_checked = true;
 }
 

@@ -519,7 +519,7 @@ struct ProofRun {
   bool lastcol_failed();
   // the early trace check (trace_stage -> composition_stage / the paired group)
   bool pre_checked = false;
-  void early_check_launch(uint32_t* dflag);
+  void early_check_launch(uint32_t* dflag, hipStream_t s);
   bool early_check_failed();
   bool h_partial = false;  // a host trace of which only this rank's columns were uploaded
   // stage sessions (zkp_session_*): the caller's channel draws every coefficient, so
