@@ -186,6 +186,8 @@ __device__ __forceinline__ void bfly2(felt& x0, felt& y0, felt w0, felt& x1, fel
 // DIF last pass, lo = 0); its round over them has jb = 0, so every twiddle of
 // stage 0, half of stage 1 and a quarter of stage 2 is 1 and those products are
 // skipped. A template flag, so the other passes keep their register budget.
+// (5 waves/SIMD for the 6-stage passes spills 4-10 VGPRs and is slower:
+// profiles/r05_ab_ntt_5waves_not_adopted.txt)
 template <bool DIT, int NT, int KC, bool SMALL>
 __global__ __launch_bounds__(NT) void k_ntt8(Ntt8Args a) {
   constexpr int E = NT * 8;

@@ -170,7 +170,9 @@ void ProofRun::trace_stage(const zkp_felt* h_trace) {
     }
     // MiMC: the trace against its transitions and assertions (k_mimc_check), read by
     // composition_stage to choose the derived last column (LastCol)
-    const bool mimc_check = allow_shortcuts && air.id == ZKP_AIR_MIMC && w == 1;
+    // (world 1: a sharded rank would check the whole replicated trace, 56 us of extra
+    // work at C4 for every valid proof; sharded proofs keep the all-gathered LastCol flags)
+    const bool mimc_check = allow_shortcuts && air.id == ZKP_AIR_MIMC && w == 1 && R == 1;
     const bool piped = h_trace && grp.size() > 1;
     const size_t G = grp.size();
     if (piped) {  // the copy stream starts after everything already queued
