@@ -1,0 +1,49 @@
+#!/usr/bin/env python3
+"""Summary of a `rocprofv3 --kernel-trace` run of the judged bench command (profiles/):
+the dominant kernel's dispatches of the headline workload, picked by shape from the
+trace (the same command also runs the C3 leg, the reference flow, the session and
+concurrent legs) on the headline context's stream (the stream of the first such
+dispatch: the concurrent leg's three contexts overlap each other's kernels on their
+own streams), and their average duration, to set beside the bench line's live
+`roofline.avg_launch_ms`.
+  python scripts/judged_kernel_summary.py <run_kernel_trace.csv> [bench json line file]
+C2 ntt_dit = k_ntt8<true, 256, ...> dispatches with 512 position blocks (2^20 / 2048);
+C3 ntt_dit = k_ntt8<true, 512, 9, ...> dispatches with 64 position blocks (2^18 / 4096)."""
+import csv
+import json
+import sys
+from collections import defaultdict
+
+
+def main():
+    rows = list(csv.DictReader(open(sys.argv[1])))
+    fam = {"c2_ntt_dit": lambda r: r["Kernel_Name"].startswith("void (anonymous namespace)::k_ntt8<true, 256,")
+           and int(r["Grid_Size_Y"]) == 512,
+           "c3_ntt_dit": lambda r: r["Kernel_Name"].startswith("void (anonymous namespace)::k_ntt8<true, 512, 9,")
+           and int(r["Grid_Size_Y"]) == 64}
+    out = {}
+    for name, pred in fam.items():
+        sel = sorted((r for r in rows if pred(r)), key=lambda r: int(r["Start_Timestamp"]))
+        if not sel:
+            continue
+        every = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in sel]
+        head = sel[0]["Stream_Id"]
+        sel = [r for r in sel if r["Stream_Id"] == head]
+        ds = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in sel]
+        by = defaultdict(list)
+        for r in sel:
+            if True:
+                by[r["Kernel_Name"].split("::k_ntt8")[1].split("(")[0]].append(
+                    (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6)
+        out[name] = {"stream": head, "dispatches": len(ds), "avg_ms": round(sum(ds) / len(ds), 5) if ds else None,
+                     "all_streams": {"dispatches": len(every), "avg_ms": round(sum(every) / len(every), 5)},
+                     "by_instance": {k: {"n": len(v), "avg_ms": round(sum(v) / len(v), 5)} for k, v in by.items()}}
+    if len(sys.argv) > 2:
+        line = json.loads(open(sys.argv[2]).read().strip().splitlines()[-1])
+        out["bench_live_avg_launch_ms"] = {"c2": line["roofline"]["avg_launch_ms"],
+                                           "c3": (line.get("c3") or {}).get("roofline", {}).get("avg_launch_ms")}
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
