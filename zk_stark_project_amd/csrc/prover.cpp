@@ -138,8 +138,13 @@ void ProofRun::trace_stage(const zkp_felt* h_trace) {
     // (a column uploads in ~0.55x its LDE at C3).
     std::vector<std::pair<uint32_t, uint32_t>> grp;
     constexpr uint32_t growth = 150;  // percent (x1.25 and x2.0 slower: profiles/r03_ab_upload_groups.txt)
+    // Short traces start from >= 2^19 felts per group (8 MiB): a group's transforms are
+    // latency-bound launches below that (TrainingUpdate at bs = 50, 2^13 x 240: 9 groups
+    // of 6..54 columns became 3 of 64, 96, 80)
     if (h_trace && wd >= 4) {
-      uint32_t cw = std::max(1u, w / 40);
+      // (at least two groups: the late paired upload rides on the pipeline's side stream)
+      uint32_t cw = std::min(std::max({1u, w / 40, (uint32_t)((1ull << 19) >> std::min(logn, 19u))}),
+                             std::max(1u, wd / 2));
       for (uint32_t c = 0; c < wd;) {
         cw = std::min(cw, wd - c);
         grp.push_back({c, cw});
