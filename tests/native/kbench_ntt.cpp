@@ -14,6 +14,7 @@
 hipEvent_t Prof::get_event() { return nullptr; }
 void Prof::begin(const char*, hipStream_t, double) {}
 void Prof::end(hipStream_t) {}
+void launch_fail(int, const char*) { abort(); }
 
 __global__ void k_copy(const uint4* __restrict__ a, uint4* __restrict__ b, uint64_t n) {
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)

@@ -95,3 +95,22 @@ if __name__ == "__main__":
         exec(code, g)
         T = g["T"]
         print(f"K={K:2d} T={T:2d}", g["check"](lambda q, x: lidx_product(q, x, T)))
+
+
+def lidx_rows_of_1(q, x):
+    """csrc/ntt.hip's rows of 1 felt (11-stage passes in 256-thread blocks, 2^19-2^20):
+    slot bits 0-2 ^= q bits 3-5, slot bit 3 ^= q bit 6."""
+    return q ^ ((q >> 3) & 7) ^ (((q >> 6) & 1) << 3)
+
+
+if __name__ == "__main__":
+    for K, LOGNT in [(11, 8), (9, 8)]:
+        g = {}
+        code = open(__file__).read().split("print('parity'")[0]
+        code = code.replace("K=10; LOGNT=9", f"K={K}; LOGNT={LOGNT}")
+        code = code.replace("i*512", f"i*{1 << LOGNT}").replace("for wave in range(8)", f"for wave in range({(1 << LOGNT) // 64})")
+        exec(code, g)
+        T = g["T"]
+        lidx = (lambda q, x: lidx_rows_of_1(q, x)) if T == 1 else (lambda q, x: lidx_product(q, x, T))
+        print(f"two-pass plan K={K:2d} T={T}", g["check"](lidx))
+

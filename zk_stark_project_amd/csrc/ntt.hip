@@ -111,22 +111,47 @@ __device__ __forceinline__ felt ntt_tw(const Ntt8Args& a, uint32_t j, uint32_t p
   return a.tw[((1u << lev) - 1) + j];
 }
 
+// Tuning builds only (tests/native/kbench_ntt.cpp, never the library): ZKP_NTT_NOBFLY
+// replaces the field arithmetic of the butterflies by two cheap ops, ZKP_NTT_NOGMEM the
+// HBM loads and stores of the array data by register values, so the time of each side
+// alone can be read against the whole pass.
+#ifdef ZKP_NTT_NOGMEM
+#define NTT_LD(p) (make((uint64_t)(uintptr_t)(p), (uint64_t)threadIdx.x))
+#define NTT_ST(p, v)                                               \
+  do {                                                            \
+    const felt v_ = (v);                                          \
+    if (v_.lo == 0x123456789ull && v_.hi == 0xabcdefull) *(p) = v_; \
+  } while (0)
+#else
+#define NTT_LD(p) (*(p))
+#define NTT_ST(p, v) (*(p) = (v))
+#endif
+
 // Butterflies of a register round. FAST: the deferred-check forms (dmul, dadd;
 // the round's Rare decides whether it is recomputed with the exact forms,
 // FAST = false); the difference of canonical values needs no check.
+#ifdef ZKP_NTT_NOBFLY
+template <bool FAST>
+__device__ __forceinline__ felt bmul(felt a, felt b, Rare& q) { return make(a.lo ^ b.lo, a.hi ^ b.hi); }
+template <bool FAST>
+__device__ __forceinline__ felt badd(felt a, felt b, Rare& q) { return make(a.lo + b.lo, a.hi + b.hi); }
+__device__ __forceinline__ felt nsub(felt a, felt b) { return make(a.lo - b.lo, a.hi - b.hi); }
+#else
 template <bool FAST>
 __device__ __forceinline__ felt bmul(felt a, felt b, Rare& q) { return dmul<FAST>(a, b, q); }
 template <bool FAST>
 __device__ __forceinline__ felt badd(felt a, felt b, Rare& q) { return dadd<FAST>(a, b, q); }
+__device__ __forceinline__ felt nsub(felt a, felt b) { return sub(a, b); }
+#endif
 
 template <bool DIT, bool FAST>
 __device__ __forceinline__ void bfly(felt& x, felt& y, felt w, Rare& q) {
   if (DIT) {
     felt t = bmul<FAST>(y, w, q);
-    y = sub(x, t);
+    y = nsub(x, t);
     x = badd<FAST>(x, t, q);
   } else {
-    felt d = sub(x, y);
+    felt d = nsub(x, y);
     x = badd<FAST>(x, y, q);
     y = bmul<FAST>(d, w, q);
   }
@@ -135,7 +160,7 @@ __device__ __forceinline__ void bfly(felt& x, felt& y, felt w, Rare& q) {
 // butterfly with twiddle 1 (no product)
 template <bool DIT, bool FAST>
 __device__ __forceinline__ void bfly1(felt& x, felt& y, Rare& q) {
-  felt d = sub(x, y);
+  felt d = nsub(x, y);
   x = badd<FAST>(x, y, q);
   y = d;
 }
@@ -161,7 +186,7 @@ struct NttRounds {
 // each carry consumer sits two instructions after its producer
 template <bool DIT, bool FAST>
 __device__ __forceinline__ void bfly2(felt& x0, felt& y0, felt w0, felt& x1, felt& y1, felt w1, Rare& q) {
-#if defined(__HIP_DEVICE_COMPILE__)
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(ZKP_NTT_NOBFLY)
   auto mx2 = [&](felt a, felt b, felt c, felt d, felt& ab, felt& cd) {
     if constexpr (FAST) fpd::mul_x2_z(a, b, c, d, ab, cd, q);
     else fpd::mul_x2(a, b, c, d, ab, cd);
@@ -196,7 +221,7 @@ __global__ __launch_bounds__(NT) void k_ntt8(Ntt8Args a) {
   constexpr uint32_t LOGNT = NT == 1024 ? 10 : (NT == 512 ? 9 : 8);
   constexpr uint32_t logT = LOGNT + 3 - KC;  // E = NT * 8 elements per block
   constexpr uint32_t T = 1u << logT;
-  static_assert(T >= 4, "the LDS swizzle needs rows of >= 4 felts");
+  static_assert(T == 1 || T >= 4, "the LDS swizzles take rows of 1 or >= 4 felts");
   const uint32_t Tl = 1u << a.logTl, lo = a.lo;
   // LDS rows of T felts (T >= 8), XOR-swizzled by the row's low 3 bits: a wave's
   // 8-lane groups then hit 8 distinct 16-B bank slots both when lanes walk a row
@@ -211,8 +236,15 @@ __global__ __launch_bounds__(NT) void k_ntt8(Ntt8Args a) {
   // the staged column walks (checked exhaustively by tests/native/lds_swizzle.py).
   // (Fully conflict-free layouts for the 8-felt and >= 32-felt rows exist —
   // tests/native/lds_swizzle.py — but measured no faster: DESIGN.md §4.)
+  // Rows of 1 felt (11-stage passes in 256-thread blocks: one 2048-element group per
+  // block): the 16-B slot bits 0-2 are XORed with q bits 3-5 and bit 3 with q bit 6, so
+  // every round of both directions and the staged walk are conflict-free (checked by
+  // tests/native/lds_swizzle.py's T = 1 model).
   auto lidx = [](uint32_t q, uint32_t x) -> uint32_t {
-    if constexpr (T >= 8) {
+    if constexpr (T == 1) {
+      (void)x;
+      return q ^ ((q >> 3) & 7u) ^ (((q >> 6) & 1u) << 3);
+    } else if constexpr (T >= 8) {
       return q * T + (x ^ (q & 7u));
     } else {
       const uint32_t b1 = (q >> 1) & 1u, b23 = ((q >> 2) ^ (q >> 3)) & 1u, b25 = ((q >> 2) ^ (q >> 5)) & 1u;
@@ -245,6 +277,8 @@ __global__ __launch_bounds__(NT) void k_ntt8(Ntt8Args a) {
   // Passes whose groups have < 8 contiguous felts (lo < 3, e.g. the first DIT
   // pass) would make every lane of a direct load/store touch its own 128-B
   // line; those go through LDS in (ll, q, hl) order, contiguous along the wave.
+  // (rows of 1: loading each lane's 8 contiguous felts directly instead, 128 B per lane,
+  // was slower: profiles/r05_kbench_ntt_two_pass.txt)
   const bool staged = a.logTl < (T >= 8 ? 3u : 2u);  // rows of 4: 64-B runs go direct
   auto staged_elem = [&](uint32_t e, uint32_t& slot) -> uint32_t {
     uint32_t ll = e & (Tl - 1), rest = e >> a.logTl;
@@ -260,8 +294,8 @@ __global__ __launch_bounds__(NT) void k_ntt8(Ntt8Args a) {
       for (int i = 0; i < 8; i++) {
         uint32_t slot;
         uint32_t ad = staged_elem(tid + i * NT, slot);
-        felt v = src[ad];
-        if (scale) v = bmul<FAST>(v, scale[ad], q);
+        felt v = NTT_LD(src + ad);
+        if (scale) v = bmul<FAST>(v, NTT_LD(scale + ad), q);
         lds[slot] = v;
       }
     };
@@ -304,8 +338,8 @@ __global__ __launch_bounds__(NT) void k_ntt8(Ntt8Args a) {
       uint32_t c = (extra << LOGNT) | tr;
       if (first && !staged) {  // straight from HBM (coalesced along gg), coset scale fused
         uint32_t ad = gaddr(coord_gg(m, tr), coord_q(m, tr));
-        felt v = src[ad];
-        if (scale) v = bmul<FAST>(v, scale[ad], qq);
+        felt v = NTT_LD(src + ad);
+        if (scale) v = bmul<FAST>(v, NTT_LD(scale + ad), qq);
         x[m] = v;
       } else {
         x[m] = lds[lidx(coord_q(m, tr), coord_gg(m, tr))];
@@ -411,7 +445,7 @@ __global__ __launch_bounds__(NT) void k_ntt8(Ntt8Args a) {
     if (!last || staged) __syncthreads();  // everyone has read this round's slots
 #pragma unroll
     for (int m = 0; m < 8; m++) {
-      if (last && !staged) dst[gaddr(coord_gg(m, tid), coord_q(m, tid))] = x[m];  // straight to HBM
+      if (last && !staged) NTT_ST(dst + gaddr(coord_gg(m, tid), coord_q(m, tid)), x[m]);  // straight to HBM
       else lds[lidx(coord_q(m, tid), coord_gg(m, tid))] = x[m];
     }
     if (DIT) b0 += rb;
@@ -422,7 +456,7 @@ __global__ __launch_bounds__(NT) void k_ntt8(Ntt8Args a) {
     for (int i = 0; i < 8; i++) {
       uint32_t slot;
       uint32_t ad = staged_elem(tid + i * NT, slot);
-      dst[ad] = lds[slot];
+      NTT_ST(dst + ad, lds[slot]);
     }
   }
   (void)E;
@@ -520,13 +554,20 @@ void launch_ntt(Prof& prof, hipStream_t s, const NttBatch& b, uint32_t logn, boo
   // (10-stage passes for 2^19-2^20 — 512-thread blocks with rows of 4 felts, the
   // T = 4 layout of k_ntt8's lidx — measured slower than 6+6+8: DESIGN.md §4.)
   const uint32_t KMAX = (logn == 17 || logn == 18) ? 9 : 8;
+  // 2^19-2^20: two passes in 256-thread blocks, 11 stages over one contiguous
+  // 2048-element group per block (the pass with lo = 0: rows of 1 felt, staged through
+  // LDS) and the rest (8 or 9 stages) over 8 or 4 adjacent groups per block: 7 LDS rounds
+  // as before (3+3+3+2 | 3+3(+3)) and a third less HBM traffic than 6+6+8
+  // (tests/native/kbench_ntt.cpp: with the butterflies compiled out the 6+6+8 passes
+  // take 1.13 of the 1.65 ms of a 48-array 2^20 LDE, about three copies of the data).
+  const bool two11 = logn == 19 || logn == 20;
   if (logN > 28)  // k_ntt8 indexes arrays and twiddles with 32-bit element offsets
     launch_fail(ZKP_ERR_TRACE_SHAPE, "NTT domain over 2^28 points (n * blowup)");
   if (logn < LOGE) {
     launch_ntt_radix2(prof, s, b, logn, dit, tw, logN);
     return;
   }
-  uint32_t npass = (logn + KMAX - 1) / KMAX;
+  uint32_t npass = two11 ? 2 : (logn + KMAX - 1) / KMAX;
   // the dynamic-LDS attributes are per device: set them once for each device this
   // process launches on (threads of an in-process group drive different devices)
   static std::mutex attr_mu;
@@ -545,7 +586,11 @@ void launch_ntt(Prof& prof, hipStream_t s, const NttBatch& b, uint32_t logn, boo
         (const void*)k_ntt8<true, 256, 5, true>,   (const void*)k_ntt8<true, 256, 6, true>,
         (const void*)k_ntt8<true, 256, 7, true>,   (const void*)k_ntt8<true, 256, 8, true>,
         (const void*)k_ntt8<false, 256, 5, true>,  (const void*)k_ntt8<false, 256, 6, true>,
-        (const void*)k_ntt8<false, 256, 7, true>,  (const void*)k_ntt8<false, 256, 8, true>};
+        (const void*)k_ntt8<false, 256, 7, true>,  (const void*)k_ntt8<false, 256, 8, true>,
+        (const void*)k_ntt8<true, 256, 9, false>,  (const void*)k_ntt8<false, 256, 9, false>,
+        (const void*)k_ntt8<true, 256, 11, true>,  (const void*)k_ntt8<false, 256, 11, true>,
+        (const void*)k_ntt8<true, 256, 9, true>,   (const void*)k_ntt8<false, 256, 9, true>,
+        (const void*)k_ntt8<true, 256, 11, false>, (const void*)k_ntt8<false, 256, 11, false>};
     for (const void* f : fns) (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)maxb);
     const void* k9[] = {(const void*)k_ntt8<true, 512, 9, false>,  (const void*)k_ntt8<false, 512, 9, false>,
                         (const void*)k_ntt8<true, 512, 9, true>,   (const void*)k_ntt8<false, 512, 9, true>};
@@ -555,7 +600,10 @@ void launch_ntt(Prof& prof, hipStream_t s, const NttBatch& b, uint32_t logn, boo
   }
   // pass sizes: prefer multiples of 3 (whole radix-8 rounds), largest pass last
   uint32_t Ks[4] = {0, 0, 0, 0};
-  {
+  if (two11) {  // the 11-stage pass is the one with lo = 0: first for DIT, last for DIF
+    Ks[0] = dit ? 11 : logn - 11;
+    Ks[1] = dit ? logn - 11 : 11;
+  } else {
     uint32_t rem = logn;
     for (uint32_t p = 0; p < npass; p++) {
       uint32_t left = npass - p;
@@ -571,8 +619,9 @@ void launch_ntt(Prof& prof, hipStream_t s, const NttBatch& b, uint32_t logn, boo
   uint32_t s0 = 0;
   for (uint32_t p = 0; p < npass; p++) {
     uint32_t K = Ks[p];
-    // 9 stages: 512 threads x 8 = 4096 elements, rows of 8 (64 KB: 2 blocks per CU)
-    const uint32_t lognt = K >= 9 ? 9 : 8, loge = lognt + 3;
+    // 9 stages (2^17-2^18): 512 threads x 8 = 4096 elements, rows of 8 (64 KB: 2 blocks
+    // per CU); the two-pass 2^19-2^20 plan keeps 256-thread blocks (rows of 1, 4 or 8)
+    const uint32_t lognt = (K >= 9 && !two11) ? 9 : 8, loge = lognt + 3;
     Ntt8Args a;
     bool first = p == 0;
     a.src = first ? b.src : b.dst;
@@ -625,8 +674,12 @@ void launch_ntt(Prof& prof, hipStream_t s, const NttBatch& b, uint32_t logn, boo
       case 12: ZKP_NTT8(false, 256, 6); break;
       case 14: ZKP_NTT8(false, 256, 7); break;
       case 16: ZKP_NTT8(false, 256, 8); break;
-      case 19: ZKP_NTT8(true, 512, 9); break;
-      case 18: ZKP_NTT8(false, 512, 9); break;
+      case 19: if (two11) ZKP_NTT8(true, 256, 9); else ZKP_NTT8(true, 512, 9); break;
+      case 18: if (two11) ZKP_NTT8(false, 256, 9); else ZKP_NTT8(false, 512, 9); break;
+      case 23: if (!small) launch_fail(ZKP_ERR_DEVICE, "internal: 11-stage NTT pass off lo = 0");
+               ZKP_NTT8(true, 256, 11); break;
+      case 22: if (!small) launch_fail(ZKP_ERR_DEVICE, "internal: 11-stage NTT pass off lo = 0");
+               ZKP_NTT8(false, 256, 11); break;
       default: launch_fail(ZKP_ERR_DEVICE, "internal: NTT pass of an unplanned size");
     }
 #undef ZKP_NTT8
