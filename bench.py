@@ -303,6 +303,8 @@ def parse():
                     help="N=1 MiMC line: skip the C3 leg (BASELINE configs[2])")
     ap.add_argument("--no-reference-flow", dest="reference_flow", action="store_false",
                     help="N=1 MiMC line: skip the reference binary's proof step (main.rs:374-493)")
+    ap.add_argument("--no-tampered", dest="tampered", action="store_false",
+                    help="skip the tampered-trace proofs (keeps PMC passes to valid proofs)")
     ap.add_argument("--air", choices=["mimc", "agg"], default="mimc",
                     help="mimc = C2 (default, the BASELINE metric); agg = C3 GlobalUpdate (64 updates, 2^18 rows)")
     return ap.parse_args()
@@ -831,7 +833,8 @@ def main():
         headline()
         sus_n += 1
     sus_s = time.perf_counter() - t1
-    tampered = tampered_leg(ctx, wl, pub, el_in / args.steps * 1e3) if (world == 1 and not sharded) else None
+    tampered = tampered_leg(ctx, wl, pub, el_in / args.steps * 1e3) \
+        if (world == 1 and not sharded and args.tampered) else None
     # the stage-hook route (a winter-prover fork keeping Prover::prove): the same proof
     # through zkp_session_* with the host channel drawing every coefficient
     session = None if sharded else session_leg(ctx, wl, pub, tr, min(args.steps, 10))

@@ -101,6 +101,7 @@ struct Ntt8Args {
   uint32_t src_div, scale_mod;
   uint32_t logn, s0, K, lo, logT, logTl, tw_shift, nrounds;
   uint32_t rbits[4];
+  uint32_t tile_major;  // 1: deal whole position blocks to XCDs (k_ntt8)
 };
 
 // stage-major twiddles: level t holds w_{2^(t+1)}^j at tw[(2^t - 1) + j]
@@ -256,11 +257,19 @@ __global__ __launch_bounds__(NT) void k_ntt8(Ntt8Args a) {
   // 8 XCDs: with B = 8 cosets batch b = col*B + j lands on XCD j, so the
   // columns of a coset share its scale rows and every batch shares the pass's
   // twiddles in that XCD's L2 instead of refetching them per array.
-  const uint32_t bidx = blockIdx.x;
+  uint32_t bidx = blockIdx.x, tile = blockIdx.y;
+  if (a.tile_major) {
+    // dispatch order i = y * B + x goes round-robin over the 8 XCDs; XCD i % 8 takes
+    // position blocks i % 8, i % 8 + 8, ... with all B batches of each back to back, so
+    // the coefficient rows and the 8 cosets' scale rows of a block are fetched once
+    const uint32_t B = gridDim.x, i = blockIdx.y * B + blockIdx.x, k = i >> 3;
+    tile = (k / B) * 8 + (i & 7);
+    bidx = k % B;
+  }
   const felt* src = a.src + (uint64_t)(bidx / a.src_div) * a.src_stride;
   felt* dst = a.dst + (uint64_t)bidx * a.dst_stride;
   const felt* scale = a.scale ? a.scale + ((uint64_t)(bidx % a.scale_mod) << a.logn) : nullptr;
-  const uint64_t g0 = (uint64_t)blockIdx.y << logT;
+  const uint64_t g0 = (uint64_t)tile << logT;
   const uint32_t hi0 = (uint32_t)(g0 >> lo);
   const uint32_t l0 = (Tl == T) ? (uint32_t)(g0 & ((1ull << lo) - 1)) : 0;
   const uint32_t qmask = (1u << K) - 1;
@@ -619,9 +628,11 @@ void launch_ntt(Prof& prof, hipStream_t s, const NttBatch& b, uint32_t logn, boo
   uint32_t s0 = 0;
   for (uint32_t p = 0; p < npass; p++) {
     uint32_t K = Ks[p];
-    // 9 stages (2^17-2^18): 512 threads x 8 = 4096 elements, rows of 8 (64 KB: 2 blocks
-    // per CU); the two-pass 2^19-2^20 plan keeps 256-thread blocks (rows of 1, 4 or 8)
-    const uint32_t lognt = (K >= 9 && !two11) ? 9 : 8, loge = lognt + 3;
+    // 9 stages: 512 threads x 8 = 4096 elements, rows of 8 felts = whole 128-B lines
+    // (64 KB: 2 blocks per CU, the same 4 waves per SIMD as the 256-thread 9-stage pass,
+    // whose 64-B runs cost 1.7x their bytes in L2 fetches: profiles/r05_ab_ntt_k512_tmaj.txt);
+    // 11 stages: 256-thread blocks of one group (rows of 1)
+    const uint32_t lognt = K >= 9 && K != 11 ? 9 : 8, loge = lognt + 3;
     Ntt8Args a;
     bool first = p == 0;
     a.src = first ? b.src : b.dst;
@@ -651,6 +662,9 @@ void launch_ntt(Prof& prof, hipStream_t s, const NttBatch& b, uint32_t logn, boo
     }
     uint64_t groups = 1ull << (logn - K);
     dim3 grid(b.batches, (uint32_t)(groups >> a.logT));  // batch fastest (see k_ntt8)
+    // the coset LDE's first pass reads each coefficient row for 8 cosets: whole position
+    // blocks per XCD (k_ntt8) keep those reads, and the scale rows, to one fetch
+    a.tile_major = first && b.src_div > 1 && grid.y % 8 == 0;
     size_t shmem = (size_t)(1u << K) * (1u << a.logT) * sizeof(felt);
     // compulsory bytes of this launch: every distinct input array once (the
     // coefficient arrays are shared by src_div coset batches, the scale table
@@ -674,8 +688,8 @@ void launch_ntt(Prof& prof, hipStream_t s, const NttBatch& b, uint32_t logn, boo
       case 12: ZKP_NTT8(false, 256, 6); break;
       case 14: ZKP_NTT8(false, 256, 7); break;
       case 16: ZKP_NTT8(false, 256, 8); break;
-      case 19: if (two11) ZKP_NTT8(true, 256, 9); else ZKP_NTT8(true, 512, 9); break;
-      case 18: if (two11) ZKP_NTT8(false, 256, 9); else ZKP_NTT8(false, 512, 9); break;
+      case 19: if (lognt == 8) ZKP_NTT8(true, 256, 9); else ZKP_NTT8(true, 512, 9); break;
+      case 18: if (lognt == 8) ZKP_NTT8(false, 256, 9); else ZKP_NTT8(false, 512, 9); break;
       case 23: if (!small) launch_fail(ZKP_ERR_DEVICE, "internal: 11-stage NTT pass off lo = 0");
                ZKP_NTT8(true, 256, 11); break;
       case 22: if (!small) launch_fail(ZKP_ERR_DEVICE, "internal: 11-stage NTT pass off lo = 0");
