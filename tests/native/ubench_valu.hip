@@ -446,6 +446,46 @@ __global__ void k_mix(uint64_t* io) {
   for (int k = 0; k < 4; k++) { io[8 * t + k] = a[k]; io[8*t+4+k] = b[k]; }
 }
 
+// rotr16(a ^ m) as two SDWA xors (word selects) vs xor + alignbit
+__global__ void k_xor_sdwa(uint64_t* io) {
+  uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  uint32_t a[8];
+  for (int k = 0; k < 8; k++) a[k] = (uint32_t)io[8 * t + k];
+  uint32_t m = (uint32_t)t | 1;
+  for (int i = 0; i < ITERS; i++) {
+#define S(k) asm volatile("v_xor_b32_sdwa %0, %0, %1 dst_sel:WORD_0 dst_unused:UNUSED_PRESERVE src0_sel:WORD_1 src1_sel:WORD_1" : "+v"(a[k]) : "v"(m));
+    CHAIN8(S)
+#undef S
+  }
+  for (int k = 0; k < 8; k++) io[8 * t + k] = a[k];
+}
+
+__global__ void k_rot16_sdwa(uint64_t* io) {  // per op = one xor + rotr16 pair
+  uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  uint32_t a[8];
+  for (int k = 0; k < 8; k++) a[k] = (uint32_t)io[8 * t + k];
+  uint32_t m = (uint32_t)t | 1;
+  for (int i = 0; i < ITERS; i++) {
+#define S(k) { uint32_t r; asm volatile("v_xor_b32_sdwa %0, %1, %2 dst_sel:WORD_0 dst_unused:UNUSED_PRESERVE src0_sel:WORD_1 src1_sel:WORD_1\n v_xor_b32_sdwa %0, %1, %2 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:WORD_0 src1_sel:WORD_0" : "=&v"(r) : "v"(a[k]), "v"(m)); a[k] = r; }
+    CHAIN8(S)
+#undef S
+  }
+  for (int k = 0; k < 8; k++) io[8 * t + k] = a[k];
+}
+
+__global__ void k_rot16_align(uint64_t* io) {  // per op = one xor + rotr16 pair
+  uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  uint32_t a[8];
+  for (int k = 0; k < 8; k++) a[k] = (uint32_t)io[8 * t + k];
+  uint32_t m = (uint32_t)t | 1;
+  for (int i = 0; i < ITERS; i++) {
+#define S(k) asm volatile("v_xor_b32 %0, %0, %1\n v_alignbit_b32 %0, %0, %0, 16" : "+v"(a[k]) : "v"(m));
+    CHAIN8(S)
+#undef S
+  }
+  for (int k = 0; k < 8; k++) io[8 * t + k] = a[k];
+}
+
 int main(int argc, char** argv) {
   setvbuf(stdout, NULL, _IONBF, 0);
   const double ghz = argc > 1 ? atof(argv[1]) : 2.4;
@@ -503,5 +543,8 @@ int main(int argc, char** argv) {
   run("pk_add_u16", k_pk_add_u16);
   run("bfe", k_bfe);
   run("mix mad+add (per op)", k_mix);
+  run("xor_sdwa", k_xor_sdwa);
+  run("xor+rot16 sdwa (pair)", k_rot16_sdwa);
+  run("xor+rot16 align (pair)", k_rot16_align);
   return 0;
 }
