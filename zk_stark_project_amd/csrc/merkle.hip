@@ -404,8 +404,10 @@ __global__ __launch_bounds__(256) void k_merkle_leaf2(MerkleArgs a) {
   store_digest(a.nodes + ((a.L >> 1) + lane) * 8, m);
 }
 
+// (MODE 4, lazy GlobalUpdate rows: held to 128 VGPRs for 4 waves per SIMD instead of
+// the 134 and 3 waves it compiles to unbounded)
 template <int MODE, int H>
-__global__ __launch_bounds__(256) void k_merkle_lane(MerkleArgs a) {
+__global__ __launch_bounds__(256, MODE == 4 ? 4 : 1) void k_merkle_lane(MerkleArgs a) {
   const uint64_t lane = blockIdx.x * (uint64_t)256 + threadIdx.x;
   if (lane >= (a.L >> H)) return;
   uint32_t root[8];
@@ -1245,18 +1247,13 @@ __global__ __launch_bounds__(512) void k_fri_tail(FriTailArgs a) {
 }  // namespace
 
 
-// tree build by lane-subtree passes: pass 1 hashes leaves and builds H0 levels,
-// later passes build up to 4 levels each from the stored subtree roots.
-template <int MODE>
-static void merkle_pass(Prof& prof, hipStream_t s, const MerkleArgs& a, uint32_t H, const char* name, double bytes) {
-  uint64_t lanes = a.L >> H;
-  dim3 g(blocks_for(lanes));
-  switch (H) {
-    case 1: LAUNCH(prof, name, s, bytes, hipLaunchKernelGGL((k_merkle_lane<MODE, 1>), g, dim3(256), 0, s, a)); break;
-    case 2: LAUNCH(prof, name, s, bytes, hipLaunchKernelGGL((k_merkle_lane<MODE, 2>), g, dim3(256), 0, s, a)); break;
-    case 3: LAUNCH(prof, name, s, bytes, hipLaunchKernelGGL((k_merkle_lane<MODE, 3>), g, dim3(256), 0, s, a)); break;
-    default: LAUNCH(prof, name, s, bytes, hipLaunchKernelGGL((k_merkle_lane<MODE, 4>), g, dim3(256), 0, s, a)); break;
-  }
+// tree build by lane-subtree passes: each lane hashes or merges 2^H nodes of the
+// level below into one subtree root (the leaf passes H = 1, the rest H = 2)
+template <int MODE, int H>
+static void merkle_pass(Prof& prof, hipStream_t s, const MerkleArgs& a, const char* name, double bytes) {
+  if ((a.L >> H) == 0) launch_fail(ZKP_ERR_DEVICE, "internal: lane pass over fewer nodes than one subtree");
+  const dim3 g(blocks_for(a.L >> H));
+  LAUNCH(prof, name, s, bytes, hipLaunchKernelGGL((k_merkle_lane<MODE, H>), g, dim3(256), 0, s, a));
 }
 
 // upper levels: wide levels by lane passes (4 levels each), the narrow top by
@@ -1275,7 +1272,7 @@ bool merkle_upper(Prof& prof, hipStream_t s, uint32_t* nodes, uint64_t L, const 
     if (L >= (1ull << lane_min_log)) {
       // 2 levels per lane: measured faster than 3-4 (fewer live digests, more waves;
       // tests/native/kbench_merkle.cpp, profiles/r02_kbench_merkle.txt)
-      merkle_pass<2>(prof, s, a, 2, "merkle_upper", (double)L * 32.0 * 1.5);
+      merkle_pass<2, 2>(prof, s, a, "merkle_upper", (double)L * 32.0 * 1.5);
       L >>= 2;
     } else {
       uint64_t blocks = (L + 511) / 512;
@@ -1301,12 +1298,13 @@ bool launch_merkle_lde(Prof& prof, hipStream_t s, const felt* lde, uint32_t cols
   a.L = L;
   // each lane hashes 2 rows and merges them (H = 1): measured faster than deeper
   // lane subtrees, whose extra live digests cost waves (kbench_merkle.cpp)
-  const uint32_t H = L >= 2 ? 1 : 0;
+  constexpr uint32_t H = 1;
+  if (L < 2) launch_fail(ZKP_ERR_DEVICE, "internal: LDE tree of one row");
   if (gl) {  // lazy GlobalUpdate columns (wide rows: the generic lane pass)
     a.gl = *gl;
-    merkle_pass<4>(prof, s, a, H, "merkle_lde", (double)L * (gl->wi * 16.0 + 64.0));
+    merkle_pass<4, H>(prof, s, a, "merkle_lde", (double)L * (gl->wi * 16.0 + 64.0));
   } else if (lc) {  // the caller checked merkle_can_derive(cols, L)
-    if (H != 1 || cols < 2 || cols > 8) launch_fail(ZKP_ERR_DEVICE, "internal: derived-column leaf shape");
+    if (cols < 2 || cols > 8) launch_fail(ZKP_ERR_DEVICE, "internal: derived-column leaf shape");
     a.lc = *lc;
     const double bytes = (double)L * (cols * 16.0 + 48.0);
     const dim3 g(blocks_for(L >> 1));
@@ -1316,7 +1314,7 @@ bool launch_merkle_lde(Prof& prof, hipStream_t s, const felt* lde, uint32_t cols
     break;
     switch (cols) { ZKP_LEAF2D(2) ZKP_LEAF2D(3) ZKP_LEAF2D(4) ZKP_LEAF2D(5) ZKP_LEAF2D(6) ZKP_LEAF2D(7) ZKP_LEAF2D(8) }
 #undef ZKP_LEAF2D
-  } else if (H == 1 && cols <= 8) {  // rows preloaded (profiles/r03_ab_leaf_preload.txt)
+  } else if (cols <= 8) {  // rows preloaded (profiles/r03_ab_leaf_preload.txt)
     const double bytes = (double)L * (cols * 16.0 + 48.0);
     const dim3 g(blocks_for(L >> 1));
 #define ZKP_LEAF2(CC) \
@@ -1325,7 +1323,7 @@ bool launch_merkle_lde(Prof& prof, hipStream_t s, const felt* lde, uint32_t cols
                     ZKP_LEAF2(8) }
 #undef ZKP_LEAF2
   } else {
-    merkle_pass<0>(prof, s, a, H, "merkle_lde", (double)L * (cols * 16.0 + 64.0));
+    merkle_pass<0, H>(prof, s, a, "merkle_lde", (double)L * (cols * 16.0 + 64.0));
   }
   return merkle_upper(prof, s, nodes, L >> H, tail);
 }
@@ -1366,10 +1364,8 @@ bool launch_merkle_fri(Prof& prof, hipStream_t s, const felt* E, uint64_t m16, u
     if (finish) return true;
     return merkle_upper(prof, s, nodes, R >= 512 ? R / 512 : 1, tail);
   }
-  uint32_t H = 0;
-  while (H < 2 && (1ull << (H + 1)) <= R) H++;
-  merkle_pass<1>(prof, s, a, H, "merkle_fri", (double)R * (F * 16.0 + 64.0));
-  return merkle_upper(prof, s, nodes, R >> H, tail);
+  merkle_pass<1, 2>(prof, s, a, "merkle_fri", (double)R * (F * 16.0 + 64.0));  // R > 2^16
+  return merkle_upper(prof, s, nodes, R >> 2, tail);
 }
 
 void preload_merkle_module() {
@@ -1544,7 +1540,7 @@ void launch_merkle_from_shards(Prof& prof, hipStream_t s, const uint32_t* recv, 
   a.logB = logB;
   a.nodes = nodes;
   a.L = L;
-  merkle_pass<3>(prof, s, a, 2, "merkle_upper", (double)L * 32.0 * 2.5);
+  merkle_pass<3, 2>(prof, s, a, "merkle_upper", (double)L * 32.0 * 2.5);
   merkle_upper(prof, s, nodes, L >> 2, tail);
 }
 
