@@ -56,7 +56,7 @@ E, H = 16, 32  # felt and digest bytes
 # summaries that scripts/profile_round.sh writes (profiles/r0*_pmc_*.json)
 KERNEL_SYMBOL = {
     "ntt_dit": "void k_ntt8<true,", "ntt_dif": "void k_ntt8<false,", "deep": "k_deep",
-    "merkle_lde": ("void k_merkle_lane<0,", "void k_merkle_leaf2<"), "eval_mimc": "k_eval_mimc",
+    "merkle_lde": ("void k_merkle_lane<0,", "void k_merkle_lane<4,", "void k_merkle_leaf2<"), "eval_mimc": "k_eval_mimc",
     "eval_linear": ("void k_eval_linear<", "void k_eval_linear_pts<"),
 }
 # launch name -> SURVEY.md Appendix C stages whose algorithmic bytes that kernel moves.
@@ -69,7 +69,7 @@ KERNEL_STAGES = {
     "eval_mimc": ("eval",), "eval_linear": ("eval",),
 }
 UBENCH_BFLY = "profiles/r04_ubench_bfly.json"  # tests/native/ubench_bfly.hip on the box: the butterfly floor
-PMC_TAGS = ("r04", "r03", "r02_final", "r02", "r01")  # newest committed PMC summaries first (scripts/profile_round.sh)
+PMC_TAGS = ("r05", "r04", "r03", "r02_final", "r02", "r01")  # newest committed PMC summaries first (scripts/profile_round.sh)
 
 
 def stage_bytes(w: int, n: int, B: int, ce: int, C: int, rem: int = 7, F: int = 16) -> dict:
@@ -199,7 +199,7 @@ def valu_side(kernel: str, air: str, mode: str):
 def isa_mix() -> dict:
     """kernel symbol (as the rocprofv3 summaries name it) -> share of 4-cycle VALU
     instructions in its gfx950 ISA (profiles/r0*_isa_mix.json, scripts/isa_mix.py)."""
-    for name in ("r04_isa_mix.json", "r02_isa_mix.json"):  # newest first
+    for name in ("r05_isa_mix.json", "r04_isa_mix.json", "r02_isa_mix.json"):  # newest first
         path = os.path.join(ROOT, "profiles", name)
         if os.path.exists(path):
             break
