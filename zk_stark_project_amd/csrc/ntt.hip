@@ -632,7 +632,10 @@ void launch_ntt(Prof& prof, hipStream_t s, const NttBatch& b, uint32_t logn, boo
     // (64 KB: 2 blocks per CU, the same 4 waves per SIMD as the 256-thread 9-stage pass,
     // whose 64-B runs cost 1.7x their bytes in L2 fetches: profiles/r05_ab_ntt_k512_tmaj.txt);
     // 11 stages: 256-thread blocks of one group (rows of 1)
-    const uint32_t lognt = K >= 9 && K != 11 ? 9 : 8, loge = lognt + 3;
+    // (2^19-2^20 with < 8 arrays, e.g. a sharded rank's 2-column interpolation rounds beside
+    // its LDE: the 64-KB blocks wait for LDS next to the other stream's kernels — C5 rank
+    // ntt_dif 0.75 -> 2.04 ms, profiles/r05_ab_rank_c5_ntt9.txt — so those keep 256 threads)
+    const uint32_t lognt = K == 9 && (!two11 || b.batches >= 8) ? 9 : 8, loge = lognt + 3;
     Ntt8Args a;
     bool first = p == 0;
     a.src = first ? b.src : b.dst;
