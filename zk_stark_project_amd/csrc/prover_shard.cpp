@@ -185,12 +185,16 @@ felt* ProofRun::composition_exchange(felt* cint, uint64_t nR) {
 void ProofRun::composition_gather_lde(felt* slice, bool derive, uint64_t nR, uint64_t p0) {
   // column by column: the all-gather of coefficient column m (rank s's slice of
   // positions [s*nR, (s+1)*nR) lands at acoef + m*n + s*nR, i.e. the column in
-  // order) runs on the side stream while the main stream extends column m - 1
+  // order) runs on the side stream while the column before it is extended
   // (the largest exchange of a sharded proof, hidden behind the
-  // composition LDE)
-  ctx->events(C);
+  // composition LDE). The extensions alternate between the main and the copy stream:
+  // one column's batch-1 passes (2048 blocks at C4) leave the last of their ~1.6 rounds
+  // of blocks part-empty, and the next column's blocks fill it
+  ctx->events(C + 1);
   HIP_CHECK(hipEventRecord(ctx->ev_fork, st));
   HIP_CHECK(hipStreamWaitEvent(ctx->side, ctx->ev_fork, 0));
+  HIP_CHECK(hipStreamWaitEvent(ctx->copy, ctx->ev_fork, 0));
+  bool on_copy = false;
   // a derived last column (LastCol) is never extended: only the OOD reads its
   // coefficients, and a split OOD reads exactly this rank's slice of them
   const bool ood_split = (n >> std::min(logn, 11u)) >= R;  // ood_launch splits its blocks
@@ -202,10 +206,19 @@ void ProofRun::composition_gather_lde(felt* slice, bool derive, uint64_t nR, uin
     }
     cm->all_gather(ctx->side, slice + (size_t)m * nR, acoef + (size_t)m * n, nR * 16);
     HIP_CHECK(hipEventRecord(ctx->up_ev[m], ctx->side));
-    HIP_CHECK(hipStreamWaitEvent(st, ctx->up_ev[m], 0));
-    if (derive && m == C - 1) break;  // derived in the leaf pass (the OOD still reads its coefficients)
+    if (derive && m == C - 1) {  // derived in the leaf pass (the OOD still reads its coefficients)
+      HIP_CHECK(hipStreamWaitEvent(st, ctx->up_ev[m], 0));
+      break;
+    }
+    hipStream_t ls = (m & 1) ? ctx->copy : st;
+    on_copy = on_copy || ls == ctx->copy;
+    HIP_CHECK(hipStreamWaitEvent(ls, ctx->up_ev[m], 0));
     NttBatch lb{acoef + (size_t)m * n, clde + (size_t)m * Bl * n, Sj0, n, n, Bl, Bl, Bl};
-    launch_ntt(pf, st, lb, logn, true, ctx->tws(logN), logN);
+    launch_ntt(pf, ls, lb, logn, true, ctx->tws(logN), logN);
+  }
+  if (on_copy) {  // the copy stream's columns (and through them their gathers) before anything reads clde
+    HIP_CHECK(hipEventRecord(ctx->up_ev[C], ctx->copy));
+    HIP_CHECK(hipStreamWaitEvent(st, ctx->up_ev[C], 0));
   }
 }
 
