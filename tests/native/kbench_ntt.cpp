@@ -81,6 +81,27 @@ int main(int argc, char** argv) {
            2.0 * nv * 16 / (ms / 10 * 1e-3) / 1e12);
     hipFree(big);
   }
+  if (argc > 2) {  // one rank of a coset-sharded proof (C4 at 2^22): 5 batch-1 coset LDEs
+    hipStream_t st2;
+    hipStreamCreate(&st2);
+    hipEvent_t fork, join;
+    hipEventCreate(&fork); hipEventCreate(&join);
+    auto col = [&](uint32_t m, hipStream_t s) {
+      NttBatch b{src + (size_t)m * n, dst + (size_t)m * n, S, n, n, 1, 1, 1};
+      launch_ntt(pf, s, b, logn, true, tw, logN);
+    };
+    run("rank: 5 batch-1 LDEs, one stream", [&] { for (uint32_t m = 0; m < 5; m++) col(m, st); }, 10);
+    run("rank: 5 batch-1 LDEs, alternating", [&] {
+      hipEventRecord(fork, st);
+      hipStreamWaitEvent(st2, fork, 0);
+      for (uint32_t m = 0; m < 5; m++) col(m, (m & 1) ? st2 : st);
+      hipEventRecord(join, st2);
+      hipStreamWaitEvent(st, join, 0);
+    }, 10);
+    NttBatch b5{src, dst, S, n, n, 1, 1, 5};
+    run("rank: 5 columns in one batch", [&] { launch_ntt(pf, st, b5, logn, true, tw, logN); }, 10);
+    return 0;
+  }
   // composition LDE: 6 columns x 8 cosets (DIT, coset scale fused)
   NttBatch lde{src, dst, S, n, n, B, B, cols * B};
   run("DIT lde 6 cols x 8 cosets", [&] { launch_ntt(pf, st, lde, logn, true, tw, logN); }, 10);
