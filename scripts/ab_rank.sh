@@ -1,7 +1,7 @@
 #!/bin/bash
 # A/B of libzkp builds on one emulated rank (tuning only):
 #   scripts/ab_rank.sh <air> <world> <lib A> <lib B>
-# alternates A and B twice; prints kernel ms per proof, wall ms, and the NTT launches' ms.
+# alternates A and B twice; prints kernel ms per proof, wall ms, and the NTT and tree launches' ms.
 set -o pipefail
 AIR=$1; W=$2; A=$3; B=$4
 for r in 1 2; do
@@ -10,6 +10,7 @@ for r in 1 2; do
     echo "$L $(echo "$out" | python -c '
 import json,sys
 d=json.loads(sys.stdin.readline()); k=d["kernels"]
-print(d["kernel_ms_per_proof"], d["wall_ms_with_host_loopback"], "ntt_dif", k["ntt_dif"], "ntt_dit", k["ntt_dit"])')"
+print(d["kernel_ms_per_proof"], d["wall_ms_with_host_loopback"],
+      " ".join("%s=%s" % (n, k[n]["ms"]) for n in ("ntt_dit", "ntt_dif", "leaf_hash_shard", "merkle_upper") if n in k))')"
   done
 done

@@ -423,8 +423,9 @@ __global__ __launch_bounds__(256, MODE == 4 ? 4 : 1) void k_merkle_lane(MerkleAr
 // send_k[((s*Bl + jl)*rc + tc)], rr = rows / R.
 // COLS > 0 (narrow LDE rows, MODE 0): the row's felts are loaded into registers
 // before hashing (compile-time row length, see k_merkle_leaf2)
+// (MODE 4, lazy GlobalUpdate rows: held to 128 VGPRs for 4 waves per SIMD, as k_merkle_lane)
 template <int MODE, int COLS = 0, bool DERIVE = false>
-__global__ __launch_bounds__(TPB) void k_leaf_hash_shard(const felt* __restrict__ src, uint64_t n, uint32_t cols,
+__global__ __launch_bounds__(TPB, MODE == 4 ? 4 : 1) void k_leaf_hash_shard(const felt* __restrict__ src, uint64_t n, uint32_t cols,
                                                          uint32_t logBl, uint32_t logrows, uint32_t logrr,
                                                          uint32_t logK, uint32_t k, uint32_t* __restrict__ send,
                                                          LastCol lc, GuLazy gl) {
