@@ -114,3 +114,32 @@ if __name__ == "__main__":
         lidx = (lambda q, x: lidx_rows_of_1(q, x)) if T == 1 else (lambda q, x: lidx_product(q, x, T))
         print(f"two-pass plan K={K:2d} T={T}", g["check"](lidx))
 
+
+
+def lidx_r06(q, x, T):
+    """csrc/ntt.hip's layouts from round 6 on: conflict-free for every pass shape the
+    library launches (rows of 16: found by a random search over GF(2) swizzles)."""
+    if T == 1:
+        return lidx_rows_of_1(q, x)
+    if T >= 32:
+        return q * T + (x ^ (q & 15))
+    if T == 16:
+        b = lambda i: (q >> i) & 1
+        s = (b(1) ^ b(3) ^ b(4)) | ((b(0) ^ b(4) ^ b(6)) << 1) | ((b(0) ^ b(1) ^ b(2)) << 2) | ((b(0) ^ b(2)) << 3)
+        return q * T + (x ^ s)
+    if T == 8:
+        return (q ^ (((q >> 2) ^ (q >> 3)) & 1)) * T + (x ^ (q & 7))
+    return lidx_product(q, x, T)
+
+
+if __name__ == "__main__":
+    for K, LOGNT in [(5, 8), (6, 8), (7, 8), (8, 8), (9, 8), (9, 9), (11, 8)]:
+        g = {}
+        code = open(__file__).read().split("print('parity'")[0]
+        code = code.replace("K=10; LOGNT=9", f"K={K}; LOGNT={LOGNT}")
+        code = code.replace("i*512", f"i*{1 << LOGNT}").replace("for wave in range(8)", f"for wave in range({(1 << LOGNT) // 64})")
+        exec(code, g)
+        T = g["T"]
+        r = g["check"](lambda q, x: lidx_r06(q, x, T))
+        print(f"r06 K={K:2d} NT={1 << LOGNT} T={T:2d}", r)
+        assert sum(r.values()) == 0

@@ -233,3 +233,25 @@ def test_channel_stages_c2_c3(ctx):
     p = gu_prover(64, 1 << 18, opts, seed=3)
     trace = p.build_trace()
     check_by_stages(ctx, AIR_GLOBAL_UPDATE, trace.data, p.get_pub_inputs(trace).to_elements(), opts)
+
+
+def test_session_pool_trim(ctx):
+    """zkp_ctx_trim frees the idle session context; two sessions open at once and
+    closed again, a trim, then a third session still proves what zkp_prove proves."""
+    fresh = _native.Context(0)
+    try:
+        fresh.trim()  # nothing pooled yet: ZKP_OK
+    finally:
+        fresh.close()
+    opts = ProofOptions(40, 8, 4)
+    p, trace = mimc_case(1 << 10, opts)
+    pub = p.get_pub_inputs(trace).to_elements()
+    s1 = _native.Session(ctx, AIR_MIMC, 1, 1 << 10, pub, opts)
+    s2 = _native.Session(ctx, AIR_MIMC, 1, 1 << 10, pub, opts)
+    r1, r2 = s1.trace_lde(trace.data), s2.trace_lde(trace.data)
+    assert r1 == r2
+    s1.close()
+    s2.close()
+    ctx.trim()
+    ctx.trim()  # idempotent
+    check_by_stages(ctx, AIR_MIMC, trace.data, pub, opts)

@@ -25,7 +25,8 @@ int zkp_ctx_create(int device, zkp_ctx** out) {
   preload_ntt_module();
   try {
     c->pinned(1u << 20);
-    c->upload(c->buf<felt>("ring_warm", 1), c, 16);
+    const felt zero[1]{};
+    c->upload(c->buf<felt>("ring_warm", 1), zero, 16);
     HIP_CHECK(hipDeviceSynchronize());
   } catch (const ZkpFail& f) {
     delete c;

@@ -1329,8 +1329,13 @@ bool launch_merkle_lde(Prof& prof, hipStream_t s, const felt* lde, uint32_t cols
   return merkle_upper(prof, s, nodes, L >> H, tail);
 }
 
-// largest FRI layer (log2 rows) whose leaves are hashed by quads (tests/native/kbench_top.cpp tunes it)
+// largest FRI layer (log2 rows) whose leaves are hashed by quads (tuned with
+// tests/native/kbench_top.cpp, which builds this file with -DZKP_FRI_QUAD_TUNING)
+#ifdef ZKP_FRI_QUAD_TUNING
 uint32_t fri_quad_max_log = 13;
+#else
+static constexpr uint32_t fri_quad_max_log = 13;
+#endif
 
 bool launch_merkle_fri(Prof& prof, hipStream_t s, const felt* E, uint64_t m16, uint32_t logB, uint32_t F,
                        uint32_t* nodes, const MerkleTail* tail) {
@@ -1343,7 +1348,7 @@ bool launch_merkle_fri(Prof& prof, hipStream_t s, const felt* E, uint64_t m16, u
   a.nodes = nodes;
   a.L = R;
   if (F == 16 && R <= (1ull << fri_quad_max_log)) {  // profiles/r02_ab_quad_leaves.txt
-    // small layers (<= 2^12 rows): one quad of lanes per row, 64 rows and 6 levels
+    // small layers (<= 2^13 rows): one quad of lanes per row, 64 rows and 6 levels
     // per block. At 2^15 rows the quads' extra instructions made it slower
     // (72 vs 53 us); at 2^11 / 2^7 / 2^3 rows it is faster (30/22/21 vs 40/34/29 us)
     uint64_t blocks = (R + 63) / 64;

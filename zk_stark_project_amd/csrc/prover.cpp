@@ -177,7 +177,8 @@ void ProofRun::trace_stage(const zkp_felt* h_trace) {
     // composition_stage to choose the derived last column (LastCol)
     // (world 1: a sharded rank would check the whole replicated trace, 56 us of extra
     // work at C4 for every valid proof; sharded proofs keep the all-gathered LastCol flags)
-    const bool mimc_check = allow_shortcuts && air.id == ZKP_AIR_MIMC && w == 1 && R == 1;
+    // (only where LastCol can read it: blowup 16, say, has ce != B and never derives)
+    const bool mimc_check = air.id == ZKP_AIR_MIMC && w == 1 && R == 1 && lastcol_shape();
     const bool piped = h_trace && grp.size() > 1;
     const size_t G = grp.size();
     if (piped) {  // the copy stream starts after everything already queued
@@ -285,6 +286,11 @@ void ProofRun::eval_stage() {
   constraint_eval(ctx, air, logn, logB, logce, u0, cel, j0, logBl, cx, twn, dt_cc, dt_aval, tlde, comp, coef, cm);
 }
 
+bool ProofRun::lastcol_shape() const {
+  static const bool no_derive = getenv("ZKP_NO_DERIVE_LAST") != nullptr;  // A/B switch
+  return allow_shortcuts && !no_derive && logce == logB && C >= 2 && C <= 8 && cel == Bl && u0 == j0;
+}
+
 // 4. composition polynomial + commitment (CompositionPoly::new +
 // DefaultConstraintCommitment) from the evaluations in `comp`: per-CE-coset
 // interpolation, exchange of coefficient slices, ce-point DFT per coefficient,
@@ -300,11 +306,9 @@ void ProofRun::composition_stage() {
     const uint64_t nR = n >> logR, p0 = (uint64_t)rank * nR;
     // the last composition column derived in the leaf pass (LastCol): the rank's
     // LDE cosets are exactly its CE cosets, whose evaluations stay in `comp`
-    static const bool no_derive = getenv("ZKP_NO_DERIVE_LAST") != nullptr;  // A/B switch
     // a trace that fails k_mimc_check proves without it (its dropped segments would
     // not be zero); one that passes cannot raise lc_bad, which stays as the backstop
-    const bool derive = allow_shortcuts && !no_derive && logce == logB && C >= 2 && C <= 8 && cel == Bl && u0 == j0 &&
-                        !(pre_checked && early_check_failed());
+    const bool derive = lastcol_shape() && !(pre_checked && early_check_failed());
     derive_last = derive;
     if (derive) {
       lc_bad = ctx->buf<uint32_t>("lc_bad", 4);
@@ -762,7 +766,11 @@ const felt* ProofRun::l0_table() {
   const std::string key = "l0_" + std::to_string(logn) + "_" + std::to_string(logB) + "_" + std::to_string(j0) + "_" +
                           std::to_string(Bl);
   felt* t = ctx->buf<felt>(key, (size_t)Bl * n);
-  if (!ctx->have_cached(key)) launch_l0_table(pf, st, PointMap{cx + j0, twn, logn}, (uint64_t)Bl * n, inv(felt_u64(n)), t);
+  if (!ctx->have_cached(key)) {
+    const uint64_t count = (uint64_t)Bl * n;
+    felt* scratch = ctx->buf<felt>("l0_scratch", l0_scratch_felts(count, logn));
+    launch_l0_table(pf, st, PointMap{cx + j0, twn, logn}, count, inv(felt_u64(n)), t, scratch);
+  }
   return t;
 }
 

@@ -514,6 +514,8 @@ struct ProofRun {
   // derived last composition column (LastCol, constraint_stage): the segments that
   // CompositionPoly::new drops must be zero (k_comp_dft raises lc_bad otherwise)
   bool derive_last = false;
+  // the shapes on which LastCol applies at all (the CE domain is the rank's LDE cosets)
+  bool lastcol_shape() const;
   uint32_t* lc_bad = nullptr;    // this rank's flag (4 words)
   uint32_t* lc_flags = nullptr;  // sharded: every rank's flags (all-gathered)
   bool lastcol_failed();

@@ -287,7 +287,10 @@ void launch_gu_coef(Prof& prof, hipStream_t s, felt* coef, uint32_t d, uint32_t 
                     uint32_t c0, uint32_t cw, uint64_t p0, uint64_t np, const felt* cval);
 void launch_gu_lde(Prof& prof, hipStream_t s, felt* lde, uint32_t d, uint32_t logn, uint32_t logBl, felt k,
                    uint32_t c0, uint32_t cw, const felt* cval, const felt* l0);
-void launch_l0_table(Prof& prof, hipStream_t s, const PointMap& pm, uint64_t count, felt ninv, felt* out);
+// scratch: l0_scratch_felts(count, logn) felts (block products + per-coset constants)
+size_t l0_scratch_felts(uint64_t count, uint32_t logn);
+void launch_l0_table(Prof& prof, hipStream_t s, const PointMap& pm, uint64_t count, felt ninv, felt* out,
+                     felt* scratch);
 // the lazy paired columns [wi, w) of the queried rows: pos = natural LDE indices
 // (npos of them), the rows of cosets [j0, j0 + 2^logBl) held here are written
 void launch_gu_fill(Prof& prof, hipStream_t s, felt* lde, uint32_t w, uint32_t logn, uint32_t logB, uint32_t j0,
