@@ -168,6 +168,10 @@ int zkp_comm_host_create(int world, int rank, const zkp_host_transport* transpor
 void zkp_comm_destroy(zkp_comm* comm);
 int zkp_comm_rank(const zkp_comm* comm);
 int zkp_comm_world(const zkp_comm* comm);
+/* The rank count the transport itself reports: ncclCommCount for an RCCL
+ * communicator (so a run can show that RCCL saw every rank), the group size for
+ * the in-process and caller transports; -1 on error. */
+int zkp_comm_backend_world(const zkp_comm* comm);
 /* Fabric check before proving (collective; no reference counterpart): one
  * all-to-all of world blocks of block_bytes (multiple of 4) and one all-gather
  * of block_bytes per rank, each run twice on the context's stream with

@@ -36,6 +36,7 @@ def test_comm_check_local_group(world):
         t.start()
     for t in ts:
         t.join()
+    assert [c.backend_world for c in comms] == [world] * world
     for c in comms:
         c.close()
     assert errs == [None] * world
@@ -52,6 +53,7 @@ def test_comm_check_rejects_bad_block(ctx):
 def test_rccl_world1_check_and_proof(ctx):
     comm = ctx.rccl_comm(_native.rccl_unique_id(), 1, 0)
     try:
+        assert comm.backend_world == 1  # ncclCommCount
         a2a_ms, ag_ms = ctx.comm_check(comm, 4 << 20)
         assert a2a_ms > 0 and ag_ms > 0
         opts = ProofOptions(8, 8, 0)

@@ -72,7 +72,7 @@ EXPORTED = [
     "zkp_copy_to_host", "zkp_trace_lde_commit", "zkp_merkle_commit_rows", "zkp_grind",
     "zkp_set_profiling", "zkp_kernel_stats", "zkp_reset_stats", "zkp_kernel_stats_table",
     "zkp_build_mimc_trace", "zkp_prove_sharded", "zkp_comm_local_group", "zkp_comm_rccl_unique_id",
-    "zkp_comm_rccl_create", "zkp_comm_destroy", "zkp_comm_rank", "zkp_comm_world", "zkp_comm_check",
+    "zkp_comm_rccl_create", "zkp_comm_destroy", "zkp_comm_rank", "zkp_comm_world", "zkp_comm_backend_world", "zkp_comm_check",
     "zkp_prove_sharded_device",
     "zkp_verify", "zkp_build_global_update_trace", "zkp_set_profiling_kernel",
     "zkp_session_create", "zkp_session_destroy", "zkp_session_trace_lde", "zkp_eval_constraints",
@@ -167,6 +167,7 @@ def load():
         L.zkp_comm_destroy.restype = None
         L.zkp_comm_rank.argtypes = [vp]
         L.zkp_comm_world.argtypes = [vp]
+        L.zkp_comm_backend_world.argtypes = [vp]
         L.zkp_comm_check.argtypes = [vp, vp, ctypes.c_uint64, ctypes.POINTER(ctypes.c_double),
                                      ctypes.POINTER(ctypes.c_double)]
         L.zkp_verify.argtypes = [i32, ctypes.c_char_p, u64, vp, u64, popt]
@@ -234,6 +235,11 @@ class Comm:
     @property
     def world(self) -> int:
         return int(self.lib.zkp_comm_world(self.ptr))
+
+    @property
+    def backend_world(self) -> int:
+        """Ranks as the transport counts them (RCCL: ncclCommCount)."""
+        return int(self.lib.zkp_comm_backend_world(self.ptr))
 
     def close(self):
         if self.ptr:

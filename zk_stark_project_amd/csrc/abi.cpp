@@ -3,34 +3,70 @@
 // prover_shard.cpp, the stage sessions in session.cpp).
 #include "prover_internal.hpp"
 
+#include <mutex>
+
 using namespace zkpi;
+
+namespace {
+// gfx950 check once per device and process (hipGetDeviceProperties queries every
+// attribute of the device: milliseconds, paid again by every context otherwise)
+bool device_is_gfx950(int device) {
+  static std::mutex mu;
+  static std::map<int, bool> known;
+  std::lock_guard<std::mutex> lk(mu);
+  auto it = known.find(device);
+  if (it != known.end()) return it->second;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) != hipSuccess) return false;
+  const bool ok = strncmp(prop.gcnArchName, "gfx950", 6) == 0;
+  known[device] = ok;
+  return ok;
+}
+}  // namespace
 
 extern "C" {
 
 int zkp_ctx_create(int device, zkp_ctx** out) {
   if (!out) return ZKP_ERR_ARGUMENT;
   *out = nullptr;
+  // phase wall times, kept in the context's statistics as host_ctx_* rows
+  using clk = std::chrono::steady_clock;
+  auto t = clk::now();
+  std::vector<std::pair<const char*, double>> phases;
+  auto lap = [&](const char* name) {
+    const auto now = clk::now();
+    phases.emplace_back(name, std::chrono::duration<double, std::milli>(now - t).count());
+    t = now;
+  };
   int count = 0;
   if (hipGetDeviceCount(&count) != hipSuccess || count <= device || device < 0) return ZKP_ERR_DEVICE;
   if (hipSetDevice(device) != hipSuccess) return ZKP_ERR_DEVICE;
-  hipDeviceProp_t prop;
-  if (hipGetDeviceProperties(&prop, device) != hipSuccess) return ZKP_ERR_DEVICE;
-  if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) return ZKP_ERR_DEVICE;  // code objects are gfx950-only
+  if (!device_is_gfx950(device)) return ZKP_ERR_DEVICE;  // code objects are gfx950-only
+  lap("host_ctx_device_check");
   zkp_ctx* c = new_ctx(device);
   if (!c) return ZKP_ERR_DEVICE;
+  lap("host_ctx_streams");
   // the kernels' code objects, the streams' hardware queues and the pinned staging
   // buffers, ahead of the first proof (a process's first proof was ≈ 4x a warm one)
   preload_kernels_module();
   preload_merkle_module();
   preload_ntt_module();
+  lap("host_ctx_code_objects");
   try {
     c->pinned(1u << 20);
+    lap("host_ctx_pinned");
     const felt zero[1]{};
     c->upload(c->buf<felt>("ring_warm", 1), zero, 16);
-    HIP_CHECK(hipDeviceSynchronize());
+    drain_streams(c);  // this context's streams only (not other contexts' proofs in flight)
+    lap("host_ctx_first_copy");
   } catch (const ZkpFail& f) {
     delete c;
     return f.code;
+  }
+  for (auto& ph : phases) {
+    auto& st = c->stats[ph.first];
+    st.launches += 1;
+    st.ms += ph.second;
   }
   *out = c;
   return ZKP_OK;

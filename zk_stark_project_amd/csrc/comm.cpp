@@ -121,6 +121,11 @@ struct RcclComm : zkp_comm {
     if (c) (void)ncclCommAbort(c);
     c = nullptr;
   }
+  int backend_world() const override {
+    int n = -1;
+    if (!c || ncclCommCount(c, &n) != ncclSuccess) return -1;
+    return n;
+  }
   ~RcclComm() override {
     if (c) (void)ncclCommDestroy(c);
     if (cs) (void)hipStreamSynchronize(cs);

@@ -29,6 +29,8 @@ struct zkp_comm {
   virtual void all_gather(hipStream_t st, const void* send, void* recv, size_t bytes) = 0;
   // called when this rank's proof fails, so that peers blocked in a collective return
   virtual void abort() {}
+  // the rank count the transport itself reports (RCCL: ncclCommCount), or -1 on error
+  virtual int backend_world() const { return world; }
 };
 
 struct CommError : std::runtime_error {

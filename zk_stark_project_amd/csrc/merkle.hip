@@ -97,6 +97,73 @@ __device__ __forceinline__ felt gu_lazy_value(const GuLazy& gl, const felt* base
   return add(kd, mul(gl.cval[ic], l));
 }
 
+// rows gu_row_hash takes (MODE 5): the reference's GlobalUpdate width, every paired column lazy
+static inline bool gu_row_shape(uint32_t cols, const GuLazy& gl) { return cols == 120 && gl.d == 60 && gl.wi == 60; }
+
+// 4 felts -> one 64-byte BLAKE3 message block
+__device__ __forceinline__ void pack4(const felt v[4], uint32_t m[16]) {
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    m[4 * k + 0] = (uint32_t)v[k].lo;
+    m[4 * k + 1] = (uint32_t)(v[k].lo >> 32);
+    m[4 * k + 2] = (uint32_t)v[k].hi;
+    m[4 * k + 3] = (uint32_t)(v[k].hi >> 32);
+  }
+}
+
+// A lazy GlobalUpdate row of the reference shape (120 felts, columns 0..59 stored and
+// 60..119 derived from them: d = wi = 60). Its two BLAKE3 chunks (columns 0..63 and
+// 64..119) are independent chains until their parent node, so they are compressed
+// interleaved: chunk 1's block b (columns 64+4b..67+4b, derived from stored columns
+// 4b+4..4b+7) right after chunk 0's block b+1, which holds exactly those columns. Every
+// stored felt is then fetched once per row (the generic getter re-read 56 of the 60 from
+// HBM for the derived half, after the row's other loads had evicted them); only chunk 0's
+// last block (columns 60..63, derived from 0..3) re-reads four.
+__device__ __forceinline__ void gu_row_hash(const GuLazy& gl, const felt* base, const felt* prev, uint64_t cstride,
+                                            felt l, uint32_t out[8]) {
+  auto derive = [&](felt cur, felt pre, uint32_t ic) {
+    const felt df = sub(cur, pre);
+    const felt kd = gl.smallk ? mul_u32(df, (uint32_t)gl.k.lo) : mul(gl.k, df);
+    return add(kd, mul(gl.cval[ic], l));
+  };
+  uint32_t cv0[8], cv1[8];
+  b3::set_iv(cv0);
+  b3::set_iv(cv1);
+  felt cur[4], prv[4];
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    cur[k] = base[k * cstride];
+    prv[k] = fp::zero();
+  }
+#pragma unroll 1
+  for (uint32_t b = 0; b < 16; b++) {
+    // next block's stored felts and their previous-row values (block 15: columns 0..3)
+    const uint32_t nb = b < 14 ? 4 * (b + 1) : 0;
+    felt nxt[4], npr[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      nxt[k] = b < 15 ? base[(nb + k) * cstride] : fp::zero();
+      npr[k] = b < 15 ? prev[(nb + k) * cstride] : fp::zero();
+    }
+    uint32_t m[16];
+    pack4(cur, m);
+    b3::compress(cv0, m, 0, 64, (b == 0 ? b3::CHUNK_START : 0u) | (b == 15 ? b3::CHUNK_END : 0u));
+    if (b >= 1 && b <= 14) {  // chunk 1, block b - 1: columns 60 + 4b + k from 4b + k
+      felt dv[4];
+#pragma unroll
+      for (int k = 0; k < 4; k++) dv[k] = derive(cur[k], prv[k], 4 * b + k);
+      pack4(dv, m);
+      b3::compress(cv1, m, 1, 64, (b == 1 ? b3::CHUNK_START : 0u) | (b == 14 ? b3::CHUNK_END : 0u));
+    }
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      cur[k] = b == 14 ? derive(nxt[k], npr[k], k) : nxt[k];  // block 15: columns 60..63
+      prv[k] = npr[k];
+    }
+  }
+  b3::parent(cv0, cv1, true, out);
+}
+
 // v[COLS-1] = (h - sum_{c<COLS-1} kappa^c v[c]) * kappa^-(COLS-1)  (LastCol; Horner
 // over the known columns: COLS-1 products)
 template <int COLS>
@@ -118,14 +185,17 @@ __device__ __forceinline__ void merkle_leaf(const MerkleArgs& a, uint64_t i, uin
     // natural row i = j + B*t' -> coset j, positions t' + k*R
     const felt* base = a.src + ((i & ((1ull << a.logB) - 1)) * 16) * a.R + (i >> a.logB);
     b3::hash_felts([&](uint32_t k) { return base[k * a.R]; }, a.cols, d);
-  } else if (MODE == 4) {  // MODE 0 with lazy GlobalUpdate columns
+  } else if (MODE == 4 || MODE == 5) {  // MODE 0 with lazy GlobalUpdate columns (5: gu_row_shape)
     const uint64_t j = i & ((1ull << a.logB) - 1), t = i >> a.logB;
     const felt* base = a.src + j * a.n + t;
     const felt* prev = a.src + j * a.n + (t == 0 ? a.n - 1 : t - 1);
     const uint64_t cstride = a.n << a.logB;
     const felt l = a.gl.l0[j * a.n + t];
-    b3::hash_felts([&](uint32_t c) { return c < a.gl.wi ? base[c * cstride] : gu_lazy_value(a.gl, base, prev, cstride, l, c); },
-                   a.cols, d);
+    if constexpr (MODE == 5)
+      gu_row_hash(a.gl, base, prev, cstride, l, d);
+    else
+      b3::hash_felts([&](uint32_t c) { return c < a.gl.wi ? base[c * cstride] : gu_lazy_value(a.gl, base, prev, cstride, l, c); },
+                     a.cols, d);
   } else if (MODE == 3) {
     // leaf i = j + B*tl sits in chunk k = tl >> logrc, source block j, row tl mod rc
     const uint64_t j = i & ((1ull << a.logB) - 1), tl = i >> a.logB;
@@ -407,7 +477,7 @@ __global__ __launch_bounds__(256) void k_merkle_leaf2(MerkleArgs a) {
 // (MODE 4, lazy GlobalUpdate rows: held to 128 VGPRs for 4 waves per SIMD instead of
 // the 134 and 3 waves it compiles to unbounded)
 template <int MODE, int H>
-__global__ __launch_bounds__(256, MODE == 4 ? 4 : 1) void k_merkle_lane(MerkleArgs a) {
+__global__ __launch_bounds__(256, MODE == 4 || MODE == 5 ? 4 : 1) void k_merkle_lane(MerkleArgs a) {
   const uint64_t lane = blockIdx.x * (uint64_t)256 + threadIdx.x;
   if (lane >= (a.L >> H)) return;
   uint32_t root[8];
@@ -425,7 +495,7 @@ __global__ __launch_bounds__(256, MODE == 4 ? 4 : 1) void k_merkle_lane(MerkleAr
 // before hashing (compile-time row length, see k_merkle_leaf2)
 // (MODE 4, lazy GlobalUpdate rows: held to 128 VGPRs for 4 waves per SIMD, as k_merkle_lane)
 template <int MODE, int COLS = 0, bool DERIVE = false>
-__global__ __launch_bounds__(TPB, MODE == 4 ? 4 : 1) void k_leaf_hash_shard(const felt* __restrict__ src, uint64_t n, uint32_t cols,
+__global__ __launch_bounds__(TPB, MODE == 4 || MODE == 5 ? 4 : 1) void k_leaf_hash_shard(const felt* __restrict__ src, uint64_t n, uint32_t cols,
                                                          uint32_t logBl, uint32_t logrows, uint32_t logrr,
                                                          uint32_t logK, uint32_t k, uint32_t* __restrict__ send,
                                                          LastCol lc, GuLazy gl) {
@@ -453,13 +523,16 @@ __global__ __launch_bounds__(TPB, MODE == 4 ? 4 : 1) void k_leaf_hash_shard(cons
     const felt* base = src + jl * n + t;
     const uint64_t cstride = n << logBl;
     b3::hash_felts([&](uint32_t c) { return base[c * cstride]; }, cols, d);
-  } else if (MODE == 4) {  // MODE 0 with lazy GlobalUpdate columns
+  } else if (MODE == 4 || MODE == 5) {  // MODE 0 with lazy GlobalUpdate columns (5: gu_row_shape)
     const felt* base = src + jl * n + t;
     const felt* prev = src + jl * n + (t == 0 ? n - 1 : t - 1);
     const uint64_t cstride = n << logBl;
     const felt l = gl.l0[jl * n + t];
-    b3::hash_felts([&](uint32_t c) { return c < gl.wi ? base[c * cstride] : gu_lazy_value(gl, base, prev, cstride, l, c); },
-                   cols, d);
+    if constexpr (MODE == 5)
+      gu_row_hash(gl, base, prev, cstride, l, d);
+    else
+      b3::hash_felts([&](uint32_t c) { return c < gl.wi ? base[c * cstride] : gu_lazy_value(gl, base, prev, cstride, l, c); },
+                     cols, d);
   } else {  // FRI row: positions t + k*rows of coset jl (16*rows per coset)
     const felt* base = src + (jl << (logrows + 4)) + t;
     b3::hash_felts([&](uint32_t kk) { return base[kk * rows]; }, cols, d);
@@ -1303,7 +1376,10 @@ bool launch_merkle_lde(Prof& prof, hipStream_t s, const felt* lde, uint32_t cols
   if (L < 2) launch_fail(ZKP_ERR_DEVICE, "internal: LDE tree of one row");
   if (gl) {  // lazy GlobalUpdate columns (wide rows: the generic lane pass)
     a.gl = *gl;
-    merkle_pass<4, H>(prof, s, a, "merkle_lde", (double)L * (gl->wi * 16.0 + 64.0));
+    if (gu_row_shape(cols, *gl))
+      merkle_pass<5, H>(prof, s, a, "merkle_lde", (double)L * (gl->wi * 16.0 + 64.0));
+    else
+      merkle_pass<4, H>(prof, s, a, "merkle_lde", (double)L * (gl->wi * 16.0 + 64.0));
   } else if (lc) {  // the caller checked merkle_can_derive(cols, L)
     if (cols < 2 || cols > 8) launch_fail(ZKP_ERR_DEVICE, "internal: derived-column leaf shape");
     a.lc = *lc;
@@ -1502,9 +1578,14 @@ void launch_leaf_hash_shard(Prof& prof, hipStream_t s, int mode, const felt* src
     break;
   if (gl) {  // lazy GlobalUpdate columns
     if (mode != 0) launch_fail(ZKP_ERR_DEVICE, "internal: lazy columns in a FRI leaf pass");
-    LAUNCH(prof, "leaf_hash_shard", s, (double)cnt * (gl->wi * 16.0 + 32.0),
-           hipLaunchKernelGGL(k_leaf_hash_shard<4>, g, dim3(TPB), 0, s, src, n, cols, logBl, logrows, logrr, logK, k,
-                              send, lcv, glv));
+    if (gu_row_shape(cols, *gl))
+      LAUNCH(prof, "leaf_hash_shard", s, (double)cnt * (gl->wi * 16.0 + 32.0),
+             hipLaunchKernelGGL(k_leaf_hash_shard<5>, g, dim3(TPB), 0, s, src, n, cols, logBl, logrows, logrr, logK,
+                                k, send, lcv, glv));
+    else
+      LAUNCH(prof, "leaf_hash_shard", s, (double)cnt * (gl->wi * 16.0 + 32.0),
+             hipLaunchKernelGGL(k_leaf_hash_shard<4>, g, dim3(TPB), 0, s, src, n, cols, logBl, logrows, logrr, logK,
+                                k, send, lcv, glv));
   } else if (lc) {  // the caller checked merkle_can_derive
     if (mode != 0 || cols < 2 || cols > 8) launch_fail(ZKP_ERR_DEVICE, "internal: derived-column shard leaf shape");
     switch (cols) { ZKP_SHARD_LEAFD(2) ZKP_SHARD_LEAFD(3) ZKP_SHARD_LEAFD(4) ZKP_SHARD_LEAFD(5)

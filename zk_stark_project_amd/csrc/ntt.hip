@@ -241,9 +241,9 @@ __global__ __launch_bounds__(NT) void k_ntt8(Ntt8Args a) {
   // block): the 16-B slot bits 0-2 are XORed with q bits 3-5 and bit 3 with q bit 6, so
   // every round of both directions and the staged walk are conflict-free (checked by
   // tests/native/lds_swizzle.py's T = 1 model).
-  // Round 6: every row length is conflict-free in the model (tests/native/lds_swizzle.py,
-  // the `r06` layouts): rows of 8 also flip the row's bit 0 with q bits 2^3, rows of 16
-  // swizzle the felt index by four parities of q bits, rows of >= 32 by q bits 0-3.
+  // Round 6: conflict-free in the model (tests/native/lds_swizzle.py, the `r06` layouts)
+  // for every row length but 16: rows of 8 also flip the row's bit 0 with q bits 2^3, rows
+  // of >= 32 swizzle the felt index by q bits 0-3.
   auto lidx = [](uint32_t q, uint32_t x) -> uint32_t {
     if constexpr (T == 1) {
       (void)x;
@@ -251,10 +251,9 @@ __global__ __launch_bounds__(NT) void k_ntt8(Ntt8Args a) {
     } else if constexpr (T >= 32) {
       return q * T + (x ^ (q & 15u));
     } else if constexpr (T == 16) {
-      // s0 = q1^q3^q4, s1 = q0^q4^q6, s2 = q0^q1^q2, s3 = q0^q2
-      const uint32_t s0 = ((q >> 1) ^ (q >> 3) ^ (q >> 4)) & 1u, s1 = (q ^ (q >> 4) ^ (q >> 6)) & 1u;
-      const uint32_t s3 = (q ^ (q >> 2)) & 1u, s2 = s3 ^ ((q >> 1) & 1u);
-      return q * T + (x ^ (s0 | (s1 << 1) | (s2 << 2) | (s3 << 3)));
+      // (a conflict-free swizzle exists, lds_swizzle.py's lidx_r06: four parities of q
+      // bits, but its index arithmetic took the 7-stage DIF pass from 100 to 134 VGPRs)
+      return q * T + (x ^ (q & 7u));
     } else if constexpr (T == 8) {
       return (q ^ (((q >> 2) ^ (q >> 3)) & 1u)) * T + (x ^ (q & 7u));
     } else {

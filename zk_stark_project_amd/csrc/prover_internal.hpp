@@ -178,6 +178,37 @@ struct zkp_ctx {
       }
       fprintf(stderr, "TL end\n");
     }
+    // the call's device-busy time: the union of its launches' [start, stop) intervals
+    // over every stream (overlapping launches counted once; idle gaps not at all),
+    // reported as the pseudo-entry "host_device_busy" (not a kernel: host_* rows are
+    // left out of the kernel tables)
+    if (prof.only.empty()) {
+      const hipEvent_t t0 = prof.pending.front().start;
+      std::vector<std::pair<float, float>> iv;
+      iv.reserve(prof.pending.size());
+      for (auto& r : prof.pending) {
+        float st = 0, en = 0;
+        HIP_CHECK(hipEventElapsedTime(&st, t0, r.start));
+        HIP_CHECK(hipEventElapsedTime(&en, t0, r.stop));
+        iv.emplace_back(st, en);
+      }
+      std::sort(iv.begin(), iv.end());
+      double busy = 0;
+      float cs = iv[0].first, ce = iv[0].second;
+      for (size_t i = 1; i < iv.size(); i++) {
+        if (iv[i].first > ce) {
+          busy += ce - cs;
+          cs = iv[i].first;
+          ce = iv[i].second;
+        } else if (iv[i].second > ce) {
+          ce = iv[i].second;
+        }
+      }
+      busy += ce - cs;
+      auto& b = stats["host_device_busy"];
+      b.launches += 1;
+      b.ms += busy;
+    }
     for (auto& r : prof.pending) {
       float ms = 0;
       HIP_CHECK(hipEventElapsedTime(&ms, r.start, r.stop));

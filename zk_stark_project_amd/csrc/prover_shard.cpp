@@ -347,4 +347,6 @@ int zkp_comm_check(zkp_ctx* ctx, zkp_comm* comm, uint64_t block_bytes, double* a
 int zkp_comm_rank(const zkp_comm* comm) { return comm ? comm->rank : -1; }
 int zkp_comm_world(const zkp_comm* comm) { return comm ? comm->world : -1; }
 
+int zkp_comm_backend_world(const zkp_comm* comm) { return comm ? comm->backend_world() : -1; }
+
 }  // extern "C"
