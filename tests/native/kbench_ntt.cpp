@@ -6,6 +6,7 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <string>
 #include <vector>
 
 #include "../../zk_stark_project_amd/csrc/zkp_internal.hpp"
@@ -81,6 +82,41 @@ int main(int argc, char** argv) {
            2.0 * nv * 16 / (ms / 10 * 1e-3) / 1e12);
     hipFree(big);
   }
+  if (argc > 2 && std::string(argv[2]) == "tu") {
+    // the reference's TrainingUpdate proof (2^13 x 240, blowup 16): one upload group of
+    // 64 columns, extended to 16 cosets, and its 64-column interpolation
+    const uint32_t tc = 64, tB = 16, tlogN = logn + 4;
+    felt *tsrc, *tdst, *tS, *ttw;
+    std::vector<felt> hs((size_t)tc * n), hS((size_t)tB * n), ht(1ull << tlogN);
+    fill(hs, 4); fill(hS, 5); fill(ht, 6);
+    hipMalloc(&tsrc, hs.size() * 16); hipMalloc(&tdst, (size_t)tc * tB * n * 16);
+    hipMalloc(&tS, hS.size() * 16); hipMalloc(&ttw, ht.size() * 16);
+    hipMemcpy(tsrc, hs.data(), hs.size() * 16, hipMemcpyHostToDevice);
+    hipMemcpy(tS, hS.data(), hS.size() * 16, hipMemcpyHostToDevice);
+    hipMemcpy(ttw, ht.data(), ht.size() * 16, hipMemcpyHostToDevice);
+    hipEvent_t a0, a1;
+    hipEventCreate(&a0); hipEventCreate(&a1);
+    auto time = [&](const char* name, auto fn) {
+      fn();
+      hipStreamSynchronize(st);
+      hipEventRecord(a0, st);
+      for (int i = 0; i < 20; i++) fn();
+      hipEventRecord(a1, st);
+      hipEventSynchronize(a1);
+      float ms;
+      hipEventElapsedTime(&ms, a0, a1);
+      std::vector<uint64_t> out((size_t)tc * n * 2);
+      hipMemcpy(out.data(), tdst, out.size() * 8, hipMemcpyDeviceToHost);
+      uint64_t ck = 0;
+      for (size_t i = 0; i < out.size(); i++) ck = ck * 0x9e3779b97f4a7c15ull + out[i];
+      printf("%-34s %8.4f ms/call  checksum %016llx\n", name, ms / 20, (unsigned long long)ck);
+    };
+    NttBatch lb{tsrc, tdst, tS, n, n, tB, tB, tc * tB};
+    time("TU: DIT lde 64 cols x 16 cosets", [&] { launch_ntt(pf, st, lb, logn, true, ttw, tlogN); });
+    NttBatch ib{tsrc, tdst, nullptr, n, n, 1, 1, tc};
+    time("TU: DIF 64 columns", [&] { launch_ntt(pf, st, ib, logn, false, ttw, tlogN); });
+    return 0;
+  }
   if (argc > 2) {  // one rank of a coset-sharded proof (C4 at 2^22): 5 batch-1 coset LDEs
     hipStream_t st2;
     hipStreamCreate(&st2);
@@ -105,6 +141,36 @@ int main(int argc, char** argv) {
   // composition LDE: 6 columns x 8 cosets (DIT, coset scale fused)
   NttBatch lde{src, dst, S, n, n, B, B, cols * B};
   run("DIT lde 6 cols x 8 cosets", [&] { launch_ntt(pf, st, lde, logn, true, tw, logN); }, 10);
+  {
+    // the same, pipelined over two streams in column chunks: pass 1 of chunk k+1 (VALU-bound)
+    // beside pass 2 of chunk k (HBM-heavier)
+    hipStream_t st2;
+    hipStreamCreate(&st2);
+    std::vector<hipEvent_t> ev(16);
+    for (auto& e : ev) hipEventCreateWithFlags(&e, hipEventDisableTiming);
+    hipEvent_t fork, join;
+    hipEventCreateWithFlags(&fork, hipEventDisableTiming);
+    hipEventCreateWithFlags(&join, hipEventDisableTiming);
+    for (uint32_t per : {1u, 2u, 3u}) {
+      char name[64];
+      snprintf(name, sizeof name, "DIT lde 6x8, pipelined %u col/chunk", per);
+      run(name, [&] {
+        hipEventRecord(fork, st);
+        hipStreamWaitEvent(st2, fork, 0);
+        uint32_t k = 0;
+        for (uint32_t c0 = 0; c0 < cols; c0 += per, k++) {
+          const uint32_t cw = c0 + per <= cols ? per : cols - c0;
+          NttBatch cb{src + (size_t)c0 * n, dst + (size_t)c0 * B * n, S, n, n, B, B, cw * B};
+          launch_ntt(pf, st, cb, logn, true, tw, logN, 0);
+          hipEventRecord(ev[k], st);
+          hipStreamWaitEvent(st2, ev[k], 0);
+          launch_ntt(pf, st2, cb, logn, true, tw, logN, 1);
+        }
+        hipEventRecord(join, st2);
+        hipStreamWaitEvent(st, join, 0);
+      }, 10);
+    }
+  }
   // trace LDE: 1 column x 8 cosets
   NttBatch lde1{src, dst, S, n, n, B, B, B};
   run("DIT lde 1 col x 8 cosets", [&] { launch_ntt(pf, st, lde1, logn, true, tw, logN); }, 20);

@@ -26,7 +26,7 @@ __device__ __forceinline__ uint32_t sel4(uint32_t q, uint32_t x0, uint32_t x1, u
 // One BLAKE3 compression (chunk counter 0, 64-byte block) by a quad: lane q
 // holds chaining-value words q (a) and 4+q (b) in and out.
 __device__ __forceinline__ void compress_quad(const uint32_t m[16], uint32_t q, uint32_t flags, uint32_t& a,
-                                              uint32_t& b, uint32_t blen = 64) {
+                                              uint32_t& b, uint32_t blen = 64, uint32_t ctr = 0) {
   constexpr uint8_t S[7][16] = {{0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15},
                                 {2, 6, 3, 10, 7, 0, 4, 13, 1, 11, 12, 5, 9, 14, 15, 8},
                                 {3, 4, 10, 12, 13, 2, 7, 14, 6, 5, 9, 0, 11, 15, 8, 1},
@@ -35,7 +35,7 @@ __device__ __forceinline__ void compress_quad(const uint32_t m[16], uint32_t q, 
                                 {9, 14, 11, 5, 8, 12, 15, 1, 13, 3, 0, 10, 2, 6, 4, 7},
                                 {11, 15, 5, 0, 1, 9, 8, 6, 14, 10, 2, 12, 3, 4, 7, 13}};
   uint32_t c = sel4(q, b3::iv(0), b3::iv(1), b3::iv(2), b3::iv(3));  // v[8..12) = IV[0..4)
-  uint32_t d = sel4(q, 0u, 0u, blen, flags);                         // counter, block_len, flags
+  uint32_t d = sel4(q, ctr, 0u, blen, flags);                        // counter, block_len, flags
 #define B3Q_G(x, y)                 \
   a = a + b + (x);                  \
   d = b3::rotr(d ^ a, 16);          \
@@ -120,6 +120,32 @@ __device__ __forceinline__ void quad_gather8(uint32_t a, uint32_t b, uint32_t ou
 // ---- the device coin and small hashes by a quad (lanes q = 0..3 of one quad, all
 // active): the serial transcript steps between the proof's stages, at ~1/4 of one
 // lane's compression latency. Lane q holds words q and 4+q of every 8-word value.
+
+// chaining value of chunk `ci` over felts [f0, f1) (<= 64) by a quad (hash_chunk's quad form):
+// lane q returns words q and 4+q
+template <typename Get>
+__device__ __forceinline__ void quad_hash_chunk(Get get, uint32_t f0, uint32_t f1, uint32_t ci, bool root, uint32_t q,
+                                                uint32_t& o0, uint32_t& o1) {
+  o0 = sel4(q, b3::iv(0), b3::iv(1), b3::iv(2), b3::iv(3));
+  o1 = sel4(q, b3::iv(4), b3::iv(5), b3::iv(6), b3::iv(7));
+  const uint32_t nblk = f1 > f0 ? (f1 - f0 + 3) / 4 : 1;
+  for (uint32_t blk = 0; blk < nblk; blk++) {
+    uint32_t m[16];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const uint32_t i = f0 + 4 * blk + k;
+      const felt v = i < f1 ? get(i) : fp::zero();
+      m[4 * k + 0] = (uint32_t)v.lo;
+      m[4 * k + 1] = (uint32_t)(v.lo >> 32);
+      m[4 * k + 2] = (uint32_t)v.hi;
+      m[4 * k + 3] = (uint32_t)(v.hi >> 32);
+    }
+    const uint32_t left = f1 - f0 - 4 * blk, cnt = left < 4 ? left : 4;
+    uint32_t fl = (blk == 0 ? b3::CHUNK_START : 0u) | (blk + 1 == nblk ? b3::CHUNK_END : 0u);
+    if (root && blk + 1 == nblk) fl |= b3::ROOT;
+    compress_quad(m, q, fl, o0, o1, f1 > f0 ? 16 * cnt : 0u, ci);
+  }
+}
 
 // Blake3_256::hash_elements of nf <= 64 felts (one chunk), get(i) read by every lane
 template <typename Get>

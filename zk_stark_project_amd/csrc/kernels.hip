@@ -567,18 +567,28 @@ constexpr uint32_t OOD_LOGE = 11;
 // A rank of a sharded proof evaluates the blocks [b0, b0 + gridDim.x) only;
 // partial[(a * gridDim.x + b - b0) * 2 + {0,1}] (the all-gathered rank blocks
 // are what k_eval_bitrev_tail reads).
+// a felt from lane (this lane + d) of the wave (d < 64; lanes past the end read their own)
+__device__ __forceinline__ felt shfl_down_f(felt v, int d) {
+  const int a = __shfl_down((int)(uint32_t)v.lo, d), b = __shfl_down((int)(uint32_t)(v.lo >> 32), d);
+  const int c = __shfl_down((int)(uint32_t)v.hi, d), e = __shfl_down((int)(uint32_t)(v.hi >> 32), d);
+  return make((uint64_t)(uint32_t)a | ((uint64_t)(uint32_t)b << 32), (uint64_t)(uint32_t)c | ((uint64_t)(uint32_t)e << 32));
+}
+
 __global__ __launch_bounds__(TPB) void k_eval_bitrev(const felt* __restrict__ arrays, uint32_t logn, uint32_t logE,
                                                      const felt* __restrict__ pw0, const felt* __restrict__ pw1,
                                                      uint32_t ntwo, uint32_t b0, felt* __restrict__ partial) {
-  __shared__ felt s0[TPB];
-  __shared__ felt s1[TPB];
+  __shared__ felt s0[TPB / 64];
+  __shared__ felt s1[TPB / 64];
   const uint32_t E = 1u << logE;
   const bool two = blockIdx.y < ntwo;  // block-uniform
   const felt* src = arrays + ((uint64_t)blockIdx.y << logn) + ((uint64_t)(b0 + blockIdx.x) << logE);
   const uint32_t t = threadIdx.x;
   // levels 0..2 in registers over the thread's 8 consecutive elements (E = 2048 = 8 * TPB),
-  // the remaining levels over the TPB thread results in LDS
+  // the next 6 levels across the wave's lanes (shuffles: no LDS banks involved; the LDS
+  // tree this replaces had 6.5 bank-conflict cycles per LDS instruction at C3), the last
+  // ones over the TPB / 64 wave results by one thread
   uint32_t l = 0, m;
+  felt r0, r1;
   if (E == 8 * TPB) {
     felt v[8];
 #pragma unroll
@@ -599,8 +609,8 @@ __global__ __launch_bounds__(TPB) void k_eval_bitrev(const felt* __restrict__ ar
     }
     {
       const felt m0 = pw0[logn - 3], m1 = pw1[logn - 3];
-      s0[t] = add(a[0], mul(m0, a[2]));
-      s1[t] = two ? add(b[0], mul(m1, b[2])) : zero();
+      r0 = add(a[0], mul(m0, a[2]));
+      r1 = two ? add(b[0], mul(m1, b[2])) : zero();
     }
     l = 3;
     m = TPB;
@@ -626,24 +636,49 @@ __global__ __launch_bounds__(TPB) void k_eval_bitrev(const felt* __restrict__ ar
         l++;
       }
     });
-    s0[t] = v0[0];
-    s1[t] = v1[0];
+    r0 = v0[0];
+    r1 = v1[0];
     m = E >= TPB ? TPB : E;
   }
-  __syncthreads();
-  for (uint32_t d = 1; d < m; d <<= 1, l++) {
-    const felt m0 = pw0[logn - 1 - l], m1 = pw1[logn - 1 - l];
-    if (t < m / (2 * d)) {
-      uint32_t p = t * 2 * d;
-      s0[p] = add(s0[p], mul(m0, s0[p + d]));
-      if (two) s1[p] = add(s1[p], mul(m1, s1[p + d]));
+  // lane t (a multiple of 2d) takes lane t + d: lanes past m hold zeros, and the lanes
+  // in between compute values nothing reads
+  for (uint32_t d = 1; d < m && d < 64; d <<= 1, l++) {
+    const felt m0 = pw0[logn - 1 - l];
+    r0 = add(r0, mul(m0, shfl_down_f(r0, (int)d)));
+    if (two) {
+      const felt m1 = pw1[logn - 1 - l];
+      r1 = add(r1, mul(m1, shfl_down_f(r1, (int)d)));
     }
-    __syncthreads();
   }
+  if ((t & 63) == 0) {
+    s0[t >> 6] = r0;
+    s1[t >> 6] = r1;
+  }
+  __syncthreads();
+  static_assert(TPB == 256, "the wave results are combined as 4 (2, 1) values");
   if (t == 0) {
+    felt a0 = s0[0], a1 = s1[0];
+    if (m > 64) {  // 4 waves (m = 256) or 2 (m = 128)
+      felt c0 = s0[2], c1 = s1[2];
+      {
+        const felt m0 = pw0[logn - 1 - l], m1 = pw1[logn - 1 - l];
+        a0 = add(a0, mul(m0, s0[1]));
+        if (two) a1 = add(a1, mul(m1, s1[1]));
+        if (m > 128) {
+          c0 = add(c0, mul(m0, s0[3]));
+          if (two) c1 = add(c1, mul(m1, s1[3]));
+        }
+        l++;
+      }
+      if (m > 128) {
+        const felt m0 = pw0[logn - 1 - l], m1 = pw1[logn - 1 - l];
+        a0 = add(a0, mul(m0, c0));
+        if (two) a1 = add(a1, mul(m1, c1));
+      }
+    }
     uint64_t o = ((uint64_t)blockIdx.y * gridDim.x + blockIdx.x) * 2;
-    partial[o] = s0[0];
-    partial[o + 1] = s1[0];
+    partial[o] = a0;
+    partial[o + 1] = two ? a1 : zero();
   }
 }
 

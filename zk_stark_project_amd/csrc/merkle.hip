@@ -474,6 +474,61 @@ __global__ __launch_bounds__(256) void k_merkle_leaf2(MerkleArgs a) {
   store_digest(a.nodes + ((a.L >> 1) + lane) * 8, m);
 }
 
+// Leaf pass of an LDE-row tree for wide rows (65..255 felts: 2-4 BLAKE3 chunks) on few
+// rows, e.g. the reference's TrainingUpdate trace (2^13 x 240 at blowup 16: 2^17 rows, which
+// a lane per row pair spreads as one 256-thread block per CU). Here a row's chunks are
+// hashed by 4 lanes at once (chunk ch by lane ch of its quad; the chunk chains are
+// independent until their parents, hash_felts' chunk tree), and an octet holds two sibling
+// rows, (2jp, t) and (2jp + 1, t). Consecutive octets take consecutive positions t of the
+// same coset pair, so each column load of a wave reads whole 128-byte lines.
+__global__ __launch_bounds__(256) void k_merkle_wide(MerkleArgs a) {
+  const uint64_t g = blockIdx.x * 256ull + threadIdx.x;
+  const uint32_t ch = threadIdx.x & 3, sib = (threadIdx.x >> 2) & 1;
+  const uint32_t logn = 63 - __builtin_clzll(a.n);
+  const uint64_t oct = g >> 3, t = oct & (a.n - 1), jp = oct >> logn;
+  const bool valid = jp < (1ull << (a.logB - 1));  // block-uniform (the grid covers L / 2 octets exactly)
+  const uint32_t nch = (a.cols + 63) / 64;
+  const uint64_t j = 2 * jp + sib, i = j + (t << a.logB);
+  uint32_t cv[8];
+  if (valid && ch < nch) {
+    const felt* base = a.src + j * a.n + t;
+    const uint64_t cstride = a.n << a.logB;
+    const uint32_t f0 = 64 * ch, f1 = f0 + 64 < a.cols ? f0 + 64 : a.cols;
+    b3::hash_chunk([&](uint32_t c) { return base[c * cstride]; }, f0, f1, ch, nch == 1, cv);
+  } else {
+#pragma unroll
+    for (int k = 0; k < 8; k++) cv[k] = 0;
+  }
+  // the row's chunk tree (nch is uniform): lane ch of a quad holds chunk ch's chaining value
+  uint32_t c1[8], root[8];
+#pragma unroll
+  for (int k = 0; k < 8; k++) c1[k] = (uint32_t)__shfl_down((int)cv[k], 1);
+  if (nch == 1) {
+#pragma unroll
+    for (int k = 0; k < 8; k++) root[k] = cv[k];
+  } else if (nch == 2) {
+    b3::parent(cv, c1, true, root);
+  } else {
+    uint32_t p[8], q[8];
+    b3::parent(cv, c1, false, p);  // lanes 0 and 2: parents of chunks (0, 1) and (2, 3)
+#pragma unroll
+    for (int k = 0; k < 8; k++) q[k] = (uint32_t)__shfl_down((int)(nch == 3 ? cv[k] : p[k]), 2);
+    b3::parent(p, q, true, root);
+  }
+  // level 1: the octet's two sibling rows
+  uint32_t sr[8];
+#pragma unroll
+  for (int k = 0; k < 8; k++) sr[k] = (uint32_t)__shfl_down((int)root[k], 4);
+  if (valid && ch == 0) {
+    store_digest(a.nodes + (a.L + i) * 8, root);
+    if (sib == 0) {
+      uint32_t m[8];
+      merge8(root, sr, m);
+      store_digest(a.nodes + ((a.L >> 1) + (i >> 1)) * 8, m);
+    }
+  }
+}
+
 // (MODE 4, lazy GlobalUpdate rows: held to 128 VGPRs for 4 waves per SIMD instead of
 // the 134 and 3 waves it compiles to unbounded)
 template <int MODE, int H>
@@ -622,53 +677,58 @@ __device__ __forceinline__ void dcoin_draw_coeffs_block(const uint32_t s[8], uin
   __syncthreads();
 }
 
-// Blake3_256::hash_elements over nf felts get(i) by a whole block: chunk c
-// (64 felts) on thread c, then the chunk tree (left subtree = largest power of
-// two) on thread 0 with the incremental stack. nf <= 64 * 32.
+// Blake3_256::hash_elements over nf felts get(i) by a whole block: chunk c (64 felts)
+// by quad c (quad_hash_chunk: a quad's compression has a ~3x shorter dependency chain
+// than one lane's, and these transcript hashes run on one block), then the chunk tree
+// (left subtree = largest power of two) by the first quad with the incremental stack.
+// nf <= 64 * 32; blockDim >= 64.
 template <typename Get>
 __device__ __forceinline__ void hash_felts_block(Get get, uint32_t nf, uint32_t out[8], uint32_t (*s_cv)[8]) {
-  const uint32_t nch = nf ? (nf + 63) / 64 : 1;
-  for (uint32_t c = threadIdx.x; c < nch; c += blockDim.x) {
-    uint32_t cv[8];
+  const uint32_t nch = nf ? (nf + 63) / 64 : 1, q = threadIdx.x & 3;
+  for (uint32_t c = threadIdx.x >> 2; c < nch; c += blockDim.x >> 2) {
+    uint32_t o0, o1;
     const uint32_t f0 = 64 * c, f1 = f0 + 64 < nf ? f0 + 64 : nf;
-    b3::hash_chunk<true>(get, f0, f1, c, nch == 1, cv);
-    for (int i = 0; i < 8; i++) s_cv[c][i] = cv[i];
+    quad_hash_chunk(get, f0, f1, c, nch == 1, q, o0, o1);
+    s_cv[c][q] = o0;
+    s_cv[c][4 + q] = o1;
   }
   __syncthreads();
-  if (threadIdx.x == 0) {
+  if (threadIdx.x < 4) {
     if (nch == 1) {
       for (int i = 0; i < 8; i++) out[i] = s_cv[0][i];
     } else {
-      // the incremental chunk-tree stack lives in s_cv itself (LDS, so no
-      // scratch): after chunk c the stack holds popcount(c + 1) <= c + 1
-      // entries, at indices below the next chunk still to be read
+      // parent(l, cur) by the quad (cur: lane q holds words q, 4+q; quad_gather8)
+      auto parent_q = [&](const uint32_t* l, uint32_t& a, uint32_t& b, bool root) {
+        uint32_t m[16];
+        quad_gather8(a, b, m + 8);
+#pragma unroll
+        for (int i = 0; i < 8; i++) m[i] = l[i];
+        a = sel4(q, b3::iv(0), b3::iv(1), b3::iv(2), b3::iv(3));
+        b = sel4(q, b3::iv(4), b3::iv(5), b3::iv(6), b3::iv(7));
+        compress_quad(m, q, b3::PARENT | (root ? b3::ROOT : 0u), a, b);
+      };
+      // the incremental chunk-tree stack lives in s_cv itself: after chunk c the stack
+      // holds popcount(c + 1) <= c + 1 entries, at indices below the next chunk to read
       uint32_t (*st)[8] = s_cv;
       int top = 0;
       for (uint32_t c = 0; c + 1 < nch; c++) {
-        uint32_t cv[8];
-        for (int i = 0; i < 8; i++) cv[i] = s_cv[c][i];
+        uint32_t a = s_cv[c][q], b = s_cv[c][4 + q];
         uint64_t total = c + 1;
         while ((total & 1) == 0) {
-          uint32_t l[8], p[8];
           --top;
-          for (int i = 0; i < 8; i++) l[i] = st[top][i];
-          b3::parent<true>(l, cv, false, p);
-          for (int i = 0; i < 8; i++) cv[i] = p[i];
+          parent_q(st[top], a, b, false);
           total >>= 1;
         }
-        for (int i = 0; i < 8; i++) st[top][i] = cv[i];
+        st[top][q] = a;
+        st[top][4 + q] = b;
         top++;
       }
-      uint32_t cv[8];
-      for (int i = 0; i < 8; i++) cv[i] = s_cv[nch - 1][i];
+      uint32_t a = s_cv[nch - 1][q], b = s_cv[nch - 1][4 + q];
       while (top > 0) {
-        uint32_t l[8], p[8];
         top--;
-        for (int i = 0; i < 8; i++) l[i] = st[top][i];
-        b3::parent<true>(l, cv, top == 0, p);
-        for (int i = 0; i < 8; i++) cv[i] = p[i];
+        parent_q(st[top], a, b, top == 0);
       }
-      for (int i = 0; i < 8; i++) out[i] = cv[i];
+      quad_gather8(a, b, out);
     }
   }
   __syncthreads();
@@ -1391,6 +1451,9 @@ bool launch_merkle_lde(Prof& prof, hipStream_t s, const felt* lde, uint32_t cols
     break;
     switch (cols) { ZKP_LEAF2D(2) ZKP_LEAF2D(3) ZKP_LEAF2D(4) ZKP_LEAF2D(5) ZKP_LEAF2D(6) ZKP_LEAF2D(7) ZKP_LEAF2D(8) }
 #undef ZKP_LEAF2D
+  } else if (cols > 64 && logB >= 1 && L <= (1ull << 20)) {  // wide rows, few of them: a quad of lanes per row
+    LAUNCH(prof, "merkle_lde", s, (double)L * (cols * 16.0 + 48.0),
+           hipLaunchKernelGGL(k_merkle_wide, dim3(blocks_for(L * 4)), dim3(256), 0, s, a));
   } else if (cols <= 8) {  // rows preloaded (profiles/r03_ab_leaf_preload.txt)
     const double bytes = (double)L * (cols * 16.0 + 48.0);
     const dim3 g(blocks_for(L >> 1));

@@ -562,8 +562,22 @@ static void launch_ntt_radix2(Prof& prof, hipStream_t s, const NttBatch& b, uint
 // radix-8 register-blocked passes: 256-thread blocks (E = 2048 elements, K <= 8)
 // for the big transforms (several blocks per CU overlap load and compute);
 // n must be >= 2^11.
+#ifndef ZKP_NTT_ONE_PASS_MAX
+#define ZKP_NTT_ONE_PASS_MAX 11  // (tuning builds set 13: see one_pass in launch_ntt)
+#endif
+
+uint32_t ntt_passes(uint32_t logn) {
+  if (logn < 11 || logn <= ZKP_NTT_ONE_PASS_MAX) return 1;
+  if (logn == 19 || logn == 20) return 2;
+#ifdef ZKP_NTT_KFIRST
+  if (logn >= 12 && logn <= 16 && logn - ZKP_NTT_KFIRST >= 5 && logn - ZKP_NTT_KFIRST <= 9) return 2;
+#endif
+  const uint32_t KMAX = (logn == 17 || logn == 18) ? 9 : 8;
+  return (logn + KMAX - 1) / KMAX;
+}
+
 void launch_ntt(Prof& prof, hipStream_t s, const NttBatch& b, uint32_t logn, bool dit, const felt* tw,
-                uint32_t logN) {
+                uint32_t logN, int only_pass) {
   const uint32_t LOGE = 11;
   // passes of up to KMAX stages. 2^17-2^18 run two passes of <= 9 stages instead
   // of three: 9-stage passes use 512-thread blocks of 4096 elements (64 KB LDS,
@@ -579,13 +593,20 @@ void launch_ntt(Prof& prof, hipStream_t s, const NttBatch& b, uint32_t logn, boo
   // (tests/native/kbench_ntt.cpp: with the butterflies compiled out the 6+6+8 passes
   // take 1.13 of the 1.65 ms of a 48-array 2^20 LDE, about three copies of the data).
   const bool two11 = logn == 19 || logn == 20;
+  // 2^11: the whole transform in one 11-stage pass (one array per 256-thread block, rows
+  // of 1 felt): one HBM read and write per array instead of 6 + 5 stages' two.
+  // (2^13 in one 1024-thread pass — 128 KB of LDS, one block per CU — was slower than
+  // 6 + 7 on the reference's TrainingUpdate proof, 2^13 x 240 at blowup 16: ntt_dit
+  // 0.76 -> 0.83 ms per proof, BENCH reference_flow.training_proof_profile; the 12- and
+  // 13-stage kernels stay for tuning builds, ZKP_NTT_ONE_PASS_MAX)
+  const bool one_pass = logn >= 11 && logn <= ZKP_NTT_ONE_PASS_MAX;
   if (logN > 28)  // k_ntt8 indexes arrays and twiddles with 32-bit element offsets
     launch_fail(ZKP_ERR_TRACE_SHAPE, "NTT domain over 2^28 points (n * blowup)");
   if (logn < LOGE) {
-    launch_ntt_radix2(prof, s, b, logn, dit, tw, logN);
+    if (only_pass <= 0) launch_ntt_radix2(prof, s, b, logn, dit, tw, logN);
     return;
   }
-  uint32_t npass = two11 ? 2 : (logn + KMAX - 1) / KMAX;
+  uint32_t npass = one_pass ? 1 : two11 ? 2 : (logn + KMAX - 1) / KMAX;
   // the dynamic-LDS attributes are per device: set them once for each device this
   // process launches on (threads of an in-process group drive different devices)
   static std::mutex attr_mu;
@@ -613,12 +634,25 @@ void launch_ntt(Prof& prof, hipStream_t s, const NttBatch& b, uint32_t logn, boo
     const void* k9[] = {(const void*)k_ntt8<true, 512, 9, false>,  (const void*)k_ntt8<false, 512, 9, false>,
                         (const void*)k_ntt8<true, 512, 9, true>,   (const void*)k_ntt8<false, 512, 9, true>};
     for (const void* f : k9) (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 4096 * 16);
+    const void* k12[] = {(const void*)k_ntt8<true, 512, 12, true>, (const void*)k_ntt8<false, 512, 12, true>};
+    for (const void* f : k12) (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 4096 * 16);
+    const void* k13[] = {(const void*)k_ntt8<true, 1024, 13, true>, (const void*)k_ntt8<false, 1024, 13, true>};
+    for (const void* f : k13) (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 8192 * 16);
     attr_devs |= 1ull << (dev & 63);
   }
   }
   // pass sizes: prefer multiples of 3 (whole radix-8 rounds), largest pass last
   uint32_t Ks[4] = {0, 0, 0, 0};
-  if (two11) {  // the 11-stage pass is the one with lo = 0: first for DIT, last for DIF
+#ifdef ZKP_NTT_KFIRST  // tuning builds only (tests/native kbench13): the lo = 0 pass takes KFIRST stages
+  if (!one_pass && !two11 && logn >= 12 && logn <= 16 && logn - ZKP_NTT_KFIRST >= 5 && logn - ZKP_NTT_KFIRST <= 9) {
+    npass = 2;
+    Ks[0] = dit ? ZKP_NTT_KFIRST : logn - ZKP_NTT_KFIRST;
+    Ks[1] = dit ? logn - ZKP_NTT_KFIRST : ZKP_NTT_KFIRST;
+  } else
+#endif
+  if (one_pass) {
+    Ks[0] = logn;
+  } else if (two11) {  // the 11-stage pass is the one with lo = 0: first for DIT, last for DIF
     Ks[0] = dit ? 11 : logn - 11;
     Ks[1] = dit ? logn - 11 : 11;
   } else {
@@ -634,9 +668,11 @@ void launch_ntt(Prof& prof, hipStream_t s, const NttBatch& b, uint32_t logn, boo
       rem -= k;
     }
   }
+  if (npass != ntt_passes(logn)) launch_fail(ZKP_ERR_DEVICE, "internal: NTT pass count");
   uint32_t s0 = 0;
-  for (uint32_t p = 0; p < npass; p++) {
+  for (uint32_t p = 0; p < npass; s0 += Ks[p], p++) {
     uint32_t K = Ks[p];
+    if (only_pass >= 0 && (uint32_t)only_pass != p) continue;
     // 9 stages: 512 threads x 8 = 4096 elements, rows of 8 felts = whole 128-B lines
     // (64 KB: 2 blocks per CU, the same 4 waves per SIMD as the 256-thread 9-stage pass,
     // whose 64-B runs cost 1.7x their bytes in L2 fetches: profiles/r05_ab_ntt_k512_tmaj.txt);
@@ -644,7 +680,7 @@ void launch_ntt(Prof& prof, hipStream_t s, const NttBatch& b, uint32_t logn, boo
     // (2^19-2^20 with < 8 arrays, e.g. a sharded rank's 2-column interpolation rounds beside
     // its LDE: the 64-KB blocks wait for LDS next to the other stream's kernels — C5 rank
     // ntt_dif 0.75 -> 2.04 ms, profiles/r05_ab_rank_c5_ntt9.txt — so those keep 256 threads)
-    const uint32_t lognt = K == 9 && (!two11 || b.batches >= 8) ? 9 : 8, loge = lognt + 3;
+    const uint32_t lognt = one_pass ? logn - 3 : K == 9 && (!two11 || b.batches >= 8) ? 9 : 8, loge = lognt + 3;
     Ntt8Args a;
     bool first = p == 0;
     a.src = first ? b.src : b.dst;
@@ -706,9 +742,20 @@ void launch_ntt(Prof& prof, hipStream_t s, const NttBatch& b, uint32_t logn, boo
                ZKP_NTT8(true, 256, 11); break;
       case 22: if (!small) launch_fail(ZKP_ERR_DEVICE, "internal: 11-stage NTT pass off lo = 0");
                ZKP_NTT8(false, 256, 11); break;
+      case 25: if (!small) launch_fail(ZKP_ERR_DEVICE, "internal: 12-stage NTT pass off lo = 0");
+               LAUNCH(prof, "ntt_dit", s, bytes,
+                      hipLaunchKernelGGL((k_ntt8<true, 512, 12, true>), grid, dim3(512), shmem, s, a)); break;
+      case 24: if (!small) launch_fail(ZKP_ERR_DEVICE, "internal: 12-stage NTT pass off lo = 0");
+               LAUNCH(prof, "ntt_dif", s, bytes,
+                      hipLaunchKernelGGL((k_ntt8<false, 512, 12, true>), grid, dim3(512), shmem, s, a)); break;
+      case 27: if (!small) launch_fail(ZKP_ERR_DEVICE, "internal: 13-stage NTT pass off lo = 0");
+               LAUNCH(prof, "ntt_dit", s, bytes,
+                      hipLaunchKernelGGL((k_ntt8<true, 1024, 13, true>), grid, dim3(1024), shmem, s, a)); break;
+      case 26: if (!small) launch_fail(ZKP_ERR_DEVICE, "internal: 13-stage NTT pass off lo = 0");
+               LAUNCH(prof, "ntt_dif", s, bytes,
+                      hipLaunchKernelGGL((k_ntt8<false, 1024, 13, true>), grid, dim3(1024), shmem, s, a)); break;
       default: launch_fail(ZKP_ERR_DEVICE, "internal: NTT pass of an unplanned size");
     }
 #undef ZKP_NTT8
-    s0 += K;
   }
 }

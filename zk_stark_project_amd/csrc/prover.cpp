@@ -9,6 +9,8 @@
 // assembles the proof bytes from the few values the verifier needs.
 #include "prover_internal.hpp"
 
+#include <mutex>
+
 using namespace zkpi;
 
 namespace zkpi {
@@ -752,6 +754,7 @@ int ProofRun::finish(uint8_t** proof, uint64_t* proof_len, zkp_transcript* tr_ou
 
   ctx->stage_end("7_queries_serialize");
   ctx->collect_prof();
+  ctx->free_retired();  // buffers a new shape outgrew (none on a warm shape)
   uint8_t* out = (uint8_t*)malloc(wr.b.size());
   if (!out) return ZKP_ERR_OOM;
   memcpy(out, wr.b.data(), wr.b.size());
@@ -866,14 +869,49 @@ void drain_streams(zkp_ctx* ctx) {
 
 void launch_fail(int code, const char* what) { throw ZkpFail{code, what}; }
 
+namespace {
+std::mutex g_stream_pool_mu;
+std::map<int, std::vector<std::array<hipStream_t, 3>>> g_stream_pool;
+constexpr size_t STREAM_POOL_MAX = 4;  // idle sets kept per device
+}  // namespace
+
+bool zkp_ctx::acquire_streams(int device, hipStream_t out[3]) {
+  std::lock_guard<std::mutex> lk(g_stream_pool_mu);
+  auto& v = g_stream_pool[device];
+  if (v.empty()) return false;
+  for (int i = 0; i < 3; i++) out[i] = v.back()[i];
+  v.pop_back();
+  return true;
+}
+
+void zkp_ctx::release_streams(int device, const hipStream_t s[3]) {
+  for (int i = 0; i < 3; i++) (void)hipStreamSynchronize(s[i]);
+  {
+    std::lock_guard<std::mutex> lk(g_stream_pool_mu);
+    auto& v = g_stream_pool[device];
+    if (v.size() < STREAM_POOL_MAX) {
+      v.push_back({s[0], s[1], s[2]});
+      return;
+    }
+  }
+  for (int i = 0; i < 3; i++) (void)hipStreamDestroy(s[i]);
+}
+
 // a context on `device` with its streams and events (nullptr on failure)
 zkp_ctx* new_ctx(int device) {
   zkp_ctx* c = new (std::nothrow) zkp_ctx();
   if (!c) return nullptr;
   c->device = device;
-  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&c->copy, hipStreamNonBlocking) != hipSuccess ||
+  hipStream_t pooled[3];
+  const bool reuse = zkp_ctx::acquire_streams(device, pooled);
+  if (reuse) {
+    c->stream = pooled[0];
+    c->side = pooled[1];
+    c->copy = pooled[2];
+  }
+  if ((!reuse && (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+                  hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess ||
+                  hipStreamCreateWithFlags(&c->copy, hipStreamNonBlocking) != hipSuccess)) ||
       hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_check, hipEventDisableTiming) != hipSuccess) {
@@ -881,8 +919,9 @@ zkp_ctx* new_ctx(int device) {
     return nullptr;
   }
   // HIP binds a stream to a hardware queue at its first dispatch: do that here,
-  // not inside the context's first proof
-  for (hipStream_t s : {c->stream, c->side, c->copy}) warm_stream(s);
+  // not inside the context's first proof (pooled streams are bound already)
+  if (!reuse)
+    for (hipStream_t s : {c->stream, c->side, c->copy}) warm_stream(s);
   return c;
 }
 

@@ -93,7 +93,11 @@ struct zkp_ctx {
     DevBuf& b = bufs[name];
     if (b.bytes < bytes) {
       auto t0 = std::chrono::steady_clock::now();
-      if (b.p) HIP_CHECK(hipFree(b.p));
+      // the smaller buffer is retired, not freed: hipFree waits for the whole device,
+      // which mid-proof would drain the queued work of this and every other stream
+      // (a new shape's first proof grows dozens of buffers); free_retired() releases
+      // them once the proof's streams are idle
+      if (b.p) retired.push_back(b.p);
       b.p = nullptr;
       HIP_CHECK(hipMalloc(&b.p, bytes));
       b.bytes = bytes;
@@ -105,6 +109,13 @@ struct zkp_ctx {
       }
     }
     return reinterpret_cast<T*>(b.p);
+  }
+  std::vector<void*> retired;  // outgrown buffers (buf()), freed by free_retired()
+  void free_retired() {
+    if (retired.empty()) return;
+    for (hipStream_t s : {stream, side, copy}) HIP_CHECK(hipStreamSynchronize(s));
+    for (void* p : retired) (void)hipFree(p);
+    retired.clear();
   }
   void sync() { HIP_CHECK(hipStreamSynchronize(stream)); }
   // true if `key` was already produced by an earlier call (the caller fills it otherwise)
@@ -337,6 +348,7 @@ struct zkp_ctx {
 
   ~zkp_ctx() {
     delete self;
+    for (void* p : retired) (void)hipFree(p);
     for (auto& kv : bufs)
       if (kv.second.p) (void)hipFree(kv.second.p);
     for (void* p : user_allocs) (void)hipFree(p);
@@ -348,10 +360,21 @@ struct zkp_ctx {
     if (ev_check) (void)hipEventDestroy(ev_check);
     if (flag_h) (void)hipHostFree(flag_h);
     if (ev_join) (void)hipEventDestroy(ev_join);
-    if (copy) (void)hipStreamDestroy(copy);
-    if (side) (void)hipStreamDestroy(side);
-    if (stream) (void)hipStreamDestroy(stream);
+    if (stream && side && copy) {
+      const hipStream_t ss[3] = {stream, side, copy};
+      release_streams(device, ss);
+    } else {
+      if (copy) (void)hipStreamDestroy(copy);
+      if (side) (void)hipStreamDestroy(side);
+      if (stream) (void)hipStreamDestroy(stream);
+    }
   }
+  // A process-wide pool of idle (stream, side, copy) sets per device: creating a
+  // context's streams binds each to a new hardware queue at its first dispatch, ≈ 8 ms
+  // for the three (BENCH reference_flow ctx_create_phases_ms); a context created after
+  // another was destroyed takes that one's bound streams instead.
+  static bool acquire_streams(int device, hipStream_t out[3]);
+  static void release_streams(int device, const hipStream_t s[3]);
 };
 
 // a context on `device` with its streams and events (nullptr on failure)

@@ -64,8 +64,12 @@ struct NttBatch {
 // Full transform over `batches` arrays of size 2^logn using the stage-major
 // twiddle table tw (level t at tw[2^t - 1 .. 2^(t+1) - 1) holds w_{2^(t+1)}^j;
 // forward table for DIT, inverse table for DIF).
+// only_pass >= 0: launch that pass of the plan alone (a caller pipelining the passes of
+// several batches over two streams: pass 1 of batch k+1 beside pass 2 of batch k);
+// ntt_passes(logn) = the number of passes of the plan (1 for the radix-2 path)
 void launch_ntt(Prof& prof, hipStream_t s, const NttBatch& b, uint32_t logn, bool dit, const felt* tw,
-                uint32_t logN);
+                uint32_t logN, int only_pass = -1);
+uint32_t ntt_passes(uint32_t logn);
 
 // ---------------------------------------------------------------- tables
 // fill levels 0..top-1 of a stage-major table whose level `top` is present
