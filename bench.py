@@ -846,9 +846,9 @@ def reference_flow_concurrent(device: int, jobs, opts, want, in_flight: int = RE
     return {"in_flight": in_flight, "flow_ms": round(ms, 3), "prove_ms_total": round(prove_ms, 3),
             "repetitions": reps,
             "proofs_identical_to_sequential": out == want,
-            "step": "8 TrainingUpdate proofs from 4 host threads (one zkp_ctx each) + the GlobalUpdate proof; "
-                    "flow_ms: each verified (zkp_verify on the proving thread), prove_ms_total: the proofs alone; "
-                    "means over the repetitions"}
+            "step": f"{len(jobs) - 1} TrainingUpdate proofs from {in_flight} host threads (one zkp_ctx each) + the "
+                    "GlobalUpdate proof; flow_ms: each verified (zkp_verify on the proving thread), prove_ms_total: "
+                    "the proofs alone; means over the repetitions"}
 
 
 def reference_flow_leg(device: int, check: bool) -> dict:
@@ -919,7 +919,7 @@ def reference_flow_leg(device: int, check: bool) -> dict:
             ctx.prove(air, tr.data, pub, opts)
         tu_stats = ctx.stats_table()
         ctx.set_profiling(False)
-        concurrent = reference_flow_concurrent(device, jobs, opts, proofs)
+        concurrent = [reference_flow_concurrent(device, jobs, opts, proofs, k) for k in (4, REF_FLOW_DEVICES)]
     finally:
         ctx.close()
     ntu = len(jobs) - 1

@@ -8,7 +8,7 @@ A=$1; B=$2; shift 2
 for r in 1 2 3; do
   for L in "$A" "$B"; do
     out=$(ZKP_LIB=$L timeout -k 10 180 python bench.py --no-cpu-baseline --no-verify --sustain-s 0 --no-concurrent \
-          --no-c3 --no-reference-flow --steps 40 "$@") || exit 1
+          --no-c3 --no-reference-flow --no-rank-emulation --steps 40 "$@") || exit 1
     echo "$L $(echo "$out" | python -c '
 import json,sys
 d=json.loads(sys.stdin.readline()); k=d["launches"]["by_kernel_ms"]

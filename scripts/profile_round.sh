@@ -13,7 +13,7 @@ shift || true
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$ROOT/gpurun_out/prof_$TAG
 mkdir -p $OUT
-ARGS="--steps 5 --warmup 2 --no-cpu-baseline --no-verify --sustain-s 0 --no-concurrent --no-c3 --no-reference-flow --no-tampered $*"
+ARGS="--steps 5 --warmup 2 --no-cpu-baseline --no-verify --sustain-s 0 --no-concurrent --no-c3 --no-reference-flow --no-rank-emulation --no-tampered $*"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- \
   python3 $ROOT/bench.py $ARGS > $OUT/trace.log 2>&1 || { echo "kernel-trace pass failed"; exit 1; }
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -o run -- \

@@ -255,7 +255,10 @@ int main(int argc, char** argv) {
   int dev = 0, cus = 0;
   CHECK(hipGetDevice(&dev));
   CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-  const int tpb = 256, blocks = cus * 20, iters = 400;
+  // --occ W: W waves per SIMD (W blocks of 4 waves per CU) instead of a full chip
+  const int occ = (argc > 2 && !strcmp(argv[1], "--occ")) ? atoi(argv[2]) : 20;
+  const int tpb = 256, blocks = cus * occ, iters = occ < 20 ? 400 * 20 / occ : 400;
+  if (occ != 20) printf("occupancy: %d wave(s) per SIMD\n", occ);
   const size_t nthr = (size_t)blocks * tpb;
   felt *d0, *d1, *tw;
   CHECK(hipMalloc(&d0, nthr * 8 * sizeof(felt)));

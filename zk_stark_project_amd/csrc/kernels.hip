@@ -567,56 +567,53 @@ constexpr uint32_t OOD_LOGE = 11;
 // A rank of a sharded proof evaluates the blocks [b0, b0 + gridDim.x) only;
 // partial[(a * gridDim.x + b - b0) * 2 + {0,1}] (the all-gathered rank blocks
 // are what k_eval_bitrev_tail reads).
-// a felt from lane (this lane + d) of the wave (d < 64; lanes past the end read their own)
-__device__ __forceinline__ felt shfl_down_f(felt v, int d) {
-  const int a = __shfl_down((int)(uint32_t)v.lo, d), b = __shfl_down((int)(uint32_t)(v.lo >> 32), d);
-  const int c = __shfl_down((int)(uint32_t)v.hi, d), e = __shfl_down((int)(uint32_t)(v.hi >> 32), d);
-  return make((uint64_t)(uint32_t)a | ((uint64_t)(uint32_t)b << 32), (uint64_t)(uint32_t)c | ((uint64_t)(uint32_t)e << 32));
-}
-
+// The array's block of E = 2^logE bit-reversed coefficients is a multilinear form in the
+// level multipliers: sum_p c[p] prod_b m_b^(bit b of p), m_b = x^(2^(logn-1-b)) for local
+// bit b (pw0 / pw1 tables), so its bits may be contracted in any order (exact field
+// arithmetic: the value is the same). With E = 2048 each thread loads elements t + 256 i
+// (i < 8: every load of a wave is 64 consecutive felts) and contracts local bits 8..10 in
+// registers; the thread bits 7..0 then pair s[t] with s[t + h] (h = 128 .. 1), so every
+// LDS access of the tree is to consecutive slots (the pairing p, p + d of the round-5 tree
+// conflicted 6.5 cycles per LDS instruction at C3).
 __global__ __launch_bounds__(TPB) void k_eval_bitrev(const felt* __restrict__ arrays, uint32_t logn, uint32_t logE,
                                                      const felt* __restrict__ pw0, const felt* __restrict__ pw1,
                                                      uint32_t ntwo, uint32_t b0, felt* __restrict__ partial) {
-  __shared__ felt s0[TPB / 64];
-  __shared__ felt s1[TPB / 64];
+  __shared__ felt s0[TPB];
+  __shared__ felt s1[TPB];
   const uint32_t E = 1u << logE;
   const bool two = blockIdx.y < ntwo;  // block-uniform
   const felt* src = arrays + ((uint64_t)blockIdx.y << logn) + ((uint64_t)(b0 + blockIdx.x) << logE);
   const uint32_t t = threadIdx.x;
-  // levels 0..2 in registers over the thread's 8 consecutive elements (E = 2048 = 8 * TPB),
-  // the next 6 levels across the wave's lanes (shuffles: no LDS banks involved; the LDS
-  // tree this replaces had 6.5 bank-conflict cycles per LDS instruction at C3), the last
-  // ones over the TPB / 64 wave results by one thread
-  uint32_t l = 0, m;
-  felt r0, r1;
+  uint32_t m, tb0;  // threads holding data, local bit of thread bit 0
   if (E == 8 * TPB) {
     felt v[8];
 #pragma unroll
-    for (int i = 0; i < 8; i++) v[i] = src[8 * t + i];
+    for (int i = 0; i < 8; i++) v[i] = src[t + TPB * i];
     felt a[4], b[4];
-    {
-      const felt m0 = pw0[logn - 1], m1 = pw1[logn - 1];
+    {  // local bit 8 (i bit 0)
+      const felt m0 = pw0[logn - 9], m1 = pw1[logn - 9];
 #pragma unroll
       for (int i = 0; i < 4; i++) a[i] = add(v[2 * i], mul(m0, v[2 * i + 1]));
       if (two)
 #pragma unroll
         for (int i = 0; i < 4; i++) b[i] = add(v[2 * i], mul(m1, v[2 * i + 1]));
     }
-    {
-      const felt m0 = pw0[logn - 2], m1 = pw1[logn - 2];
+    {  // local bit 9
+      const felt m0 = pw0[logn - 10], m1 = pw1[logn - 10];
       a[0] = add(a[0], mul(m0, a[1])); a[2] = add(a[2], mul(m0, a[3]));
       if (two) { b[0] = add(b[0], mul(m1, b[1])); b[2] = add(b[2], mul(m1, b[3])); }
     }
-    {
-      const felt m0 = pw0[logn - 3], m1 = pw1[logn - 3];
-      r0 = add(a[0], mul(m0, a[2]));
-      r1 = two ? add(b[0], mul(m1, b[2])) : zero();
+    {  // local bit 10
+      const felt m0 = pw0[logn - 11], m1 = pw1[logn - 11];
+      s0[t] = add(a[0], mul(m0, a[2]));
+      s1[t] = two ? add(b[0], mul(m1, b[2])) : zero();
     }
-    l = 3;
     m = TPB;
+    tb0 = 0;
   } else {  // smaller blocks: per = E / TPB consecutive elements per thread (or one)
     // (E < 2048: per <= 4; compile-time register indices, guarded by the runtime per)
     const uint32_t per = E >= TPB ? E / TPB : 1;
+    uint32_t l = 0;
     felt v0[4], v1[4];
     static_for<0, 4>([&](auto ii) {
       constexpr uint32_t i = decltype(ii)::value;
@@ -636,49 +633,29 @@ __global__ __launch_bounds__(TPB) void k_eval_bitrev(const felt* __restrict__ ar
         l++;
       }
     });
-    r0 = v0[0];
-    r1 = v1[0];
+    s0[t] = v0[0];
+    s1[t] = v1[0];
     m = E >= TPB ? TPB : E;
-  }
-  // lane t (a multiple of 2d) takes lane t + d: lanes past m hold zeros, and the lanes
-  // in between compute values nothing reads
-  for (uint32_t d = 1; d < m && d < 64; d <<= 1, l++) {
-    const felt m0 = pw0[logn - 1 - l];
-    r0 = add(r0, mul(m0, shfl_down_f(r0, (int)d)));
-    if (two) {
-      const felt m1 = pw1[logn - 1 - l];
-      r1 = add(r1, mul(m1, shfl_down_f(r1, (int)d)));
-    }
-  }
-  if ((t & 63) == 0) {
-    s0[t >> 6] = r0;
-    s1[t >> 6] = r1;
+    tb0 = l;
   }
   __syncthreads();
-  static_assert(TPB == 256, "the wave results are combined as 4 (2, 1) values");
-  if (t == 0) {
-    felt a0 = s0[0], a1 = s1[0];
-    if (m > 64) {  // 4 waves (m = 256) or 2 (m = 128)
-      felt c0 = s0[2], c1 = s1[2];
-      {
-        const felt m0 = pw0[logn - 1 - l], m1 = pw1[logn - 1 - l];
-        a0 = add(a0, mul(m0, s0[1]));
-        if (two) a1 = add(a1, mul(m1, s1[1]));
-        if (m > 128) {
-          c0 = add(c0, mul(m0, s0[3]));
-          if (two) c1 = add(c1, mul(m1, s1[3]));
-        }
-        l++;
-      }
-      if (m > 128) {
-        const felt m0 = pw0[logn - 1 - l], m1 = pw1[logn - 1 - l];
-        a0 = add(a0, mul(m0, c0));
-        if (two) a1 = add(a1, mul(m1, c1));
+  // thread bits from the top: s[t] += m_b * s[t + h] for t < h, b = tb0 + log2 h
+  for (uint32_t h = m >> 1; h >= 1; h >>= 1) {
+    const uint32_t lb = 31 - __builtin_clz(h);
+    if (t < h) {
+      const felt m0 = pw0[logn - 1 - tb0 - lb];
+      s0[t] = add(s0[t], mul(m0, s0[t + h]));
+      if (two) {
+        const felt m1 = pw1[logn - 1 - tb0 - lb];
+        s1[t] = add(s1[t], mul(m1, s1[t + h]));
       }
     }
+    __syncthreads();
+  }
+  if (t == 0) {
     uint64_t o = ((uint64_t)blockIdx.y * gridDim.x + blockIdx.x) * 2;
-    partial[o] = a0;
-    partial[o + 1] = two ? a1 : zero();
+    partial[o] = s0[0];
+    partial[o + 1] = two ? s1[0] : zero();
   }
 }
 

@@ -102,6 +102,7 @@ struct Ntt8Args {
   uint32_t logn, s0, K, lo, logT, logTl, tw_shift, nrounds;
   uint32_t rbits[4];
   uint32_t tile_major;  // 1: deal whole position blocks to XCDs (k_ntt8)
+  uint32_t batches, items;  // k_ntt8_pipe: batches of the pass, tiles x batches
 };
 
 // stage-major twiddles: level t holds w_{2^(t+1)}^j at tw[(2^t - 1) + j]
@@ -214,11 +215,25 @@ __device__ __forceinline__ void bfly2(felt& x0, felt& y0, felt w0, felt& x1, fel
 // skipped. A template flag, so the other passes keep their register budget.
 // (5 waves/SIMD for the 6-stage passes spills 4-10 VGPRs and is slower:
 // profiles/r05_ab_ntt_5waves_not_adopted.txt)
-template <bool DIT, int NT, int KC, bool SMALL>
-__global__ __launch_bounds__(NT) void k_ntt8(Ntt8Args a) {
+// LDS barrier of the passes: every wave's LDS operations retired, then s_barrier. No
+// vmcnt wait: the pipelined pass keeps its next tile's LDS-DMA loads in flight across
+// it (a __syncthreads() would drain them, cdna_hip_programming.md §5).
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+}
+
+// One tile of a k_ntt8 pass (block-local elements (gg, q) of batch bidx, position block
+// `tile`) in the block's LDS `lds`. PIPE: round 0 reads the tile from `lds`, where
+// k_ntt8_pipe's LDS-DMA put it (the pass has no coset scale and loads directly).
+template <bool DIT, int NT, int KC, bool SMALL, bool PIPE = false>
+__device__ __forceinline__ void ntt8_tile(const Ntt8Args& a, uint32_t bidx, uint32_t tile, felt* lds) {
   constexpr int E = NT * 8;
-  extern __shared__ felt lds[];
   constexpr uint32_t K = KC;
+  auto tile_barrier = [] {
+    if constexpr (PIPE) lds_barrier();
+    else __syncthreads();
+  };
   constexpr uint32_t LOGNT = NT == 1024 ? 10 : (NT == 512 ? 9 : 8);
   constexpr uint32_t logT = LOGNT + 3 - KC;  // E = NT * 8 elements per block
   constexpr uint32_t T = 1u << logT;
@@ -266,15 +281,6 @@ __global__ __launch_bounds__(NT) void k_ntt8(Ntt8Args a) {
   // 8 XCDs: with B = 8 cosets batch b = col*B + j lands on XCD j, so the
   // columns of a coset share its scale rows and every batch shares the pass's
   // twiddles in that XCD's L2 instead of refetching them per array.
-  uint32_t bidx = blockIdx.x, tile = blockIdx.y;
-  if (a.tile_major) {
-    // dispatch order i = y * B + x goes round-robin over the 8 XCDs; XCD i % 8 takes
-    // position blocks i % 8, i % 8 + 8, ... with all B batches of each back to back, so
-    // the coefficient rows and the 8 cosets' scale rows of a block are fetched once
-    const uint32_t B = gridDim.x, i = blockIdx.y * B + blockIdx.x, k = i >> 3;
-    tile = (k / B) * 8 + (i & 7);
-    bidx = k % B;
-  }
   const felt* src = a.src + (uint64_t)(bidx / a.src_div) * a.src_stride;
   felt* dst = a.dst + (uint64_t)bidx * a.dst_stride;
   const felt* scale = a.scale ? a.scale + ((uint64_t)(bidx % a.scale_mod) << a.logn) : nullptr;
@@ -320,7 +326,7 @@ __global__ __launch_bounds__(NT) void k_ntt8(Ntt8Args a) {
     Rare q;
     stage_in(std::true_type{}, q);
     if (scale && q.any()) stage_in(std::false_type{}, q);
-    __syncthreads();
+    tile_barrier();
   }
   uint32_t b0 = DIT ? 0 : K;
   static_for<0, NttRounds<KC>::n>([&](auto rr) {
@@ -328,7 +334,7 @@ __global__ __launch_bounds__(NT) void k_ntt8(Ntt8Args a) {
     constexpr uint32_t rb = NttRounds<KC>::bits(r);
     if (!DIT) b0 -= rb;
     constexpr bool first = r == 0, last = r + 1 == NttRounds<KC>::n;
-    if (!first) __syncthreads();
+    if (!first) tile_barrier();
     felt x[8];
     uint32_t ggs[2], qlow[2];
     // block-local coordinates (gg, q) of register m in this round (for thread tr)
@@ -354,7 +360,7 @@ __global__ __launch_bounds__(NT) void k_ntt8(Ntt8Args a) {
     for (int m = 0; m < 8; m++) {
       uint32_t extra = m >> rb, bf = m & ((1u << rb) - 1);
       uint32_t c = (extra << LOGNT) | tr;
-      if (first && !staged) {  // straight from HBM (coalesced along gg), coset scale fused
+      if (first && !staged && !PIPE) {  // straight from HBM (coalesced along gg), coset scale fused
         uint32_t ad = gaddr(coord_gg(m, tr), coord_q(m, tr));
         felt v = NTT_LD(src + ad);
         if (scale) v = bmul<FAST>(v, NTT_LD(scale + ad), qq);
@@ -460,7 +466,7 @@ __global__ __launch_bounds__(NT) void k_ntt8(Ntt8Args a) {
     Rare qq;
     round(std::true_type{}, qq);
     if (qq.any()) round(std::false_type{}, qq);
-    if (!last || staged) __syncthreads();  // everyone has read this round's slots
+    if (!last || staged) tile_barrier();  // everyone has read this round's slots
 #pragma unroll
     for (int m = 0; m < 8; m++) {
       if (last && !staged) NTT_ST(dst + gaddr(coord_gg(m, tid), coord_q(m, tid)), x[m]);  // straight to HBM
@@ -469,7 +475,7 @@ __global__ __launch_bounds__(NT) void k_ntt8(Ntt8Args a) {
     if (DIT) b0 += rb;
   });
   if (staged) {  // LDS -> HBM in the contiguous order
-    __syncthreads();
+    tile_barrier();
 #pragma unroll
     for (int i = 0; i < 8; i++) {
       uint32_t slot;
@@ -478,6 +484,70 @@ __global__ __launch_bounds__(NT) void k_ntt8(Ntt8Args a) {
     }
   }
   (void)E;
+}
+
+template <bool DIT, int NT, int KC, bool SMALL>
+__global__ __launch_bounds__(NT) void k_ntt8(Ntt8Args a) {
+  extern __shared__ felt lds[];
+  uint32_t bidx = blockIdx.x, tile = blockIdx.y;
+  if (a.tile_major) {
+    // dispatch order i = y * B + x goes round-robin over the 8 XCDs; XCD i % 8 takes
+    // position blocks i % 8, i % 8 + 8, ... with all B batches of each back to back, so
+    // the coefficient rows and the 8 cosets' scale rows of a block are fetched once
+    const uint32_t B = gridDim.x, i = blockIdx.y * B + blockIdx.x, k = i >> 3;
+    tile = (k / B) * 8 + (i & 7);
+    bidx = k % B;
+  }
+  ntt8_tile<DIT, NT, KC, SMALL>(a, bidx, tile, lds);
+}
+
+// The 9-stage pass in rows of 8 felts (512 threads, 4096 felts per tile) with direct loads
+// (2^20: DIT pass 2, DIF pass 1), software-pipelined: one persistent block per CU over the
+// pass's tiles (item = tile * batches + batch, batch fastest as in k_ntt8), two 64-KB LDS
+// buffers. While a tile's three rounds run, the next tile streams into the other buffer by
+// LDS-DMA (global_load_lds_dwordx4: no VGPRs held, so the rounds keep their registers);
+// the swizzle of k_ntt8's rows of 8 goes on the per-lane source address (the DMA writes a
+// wave's 1 KB lane-linearly).
+// TUNING BUILDS ONLY (ZKP_NTT_PIPE=1; not adopted): bit-exact, but
+// 1.68 against 1.51 ms for the C2 composition-shape LDE (profiles/r06_ab_ntt_pipe_not_adopted.txt).
+// The twiddle loads of the rounds are ordinary loads, beside which hipcc waits vmcnt(0) and
+// so drains the prefetch; and even with the loads perfectly hidden, one 512-thread block per
+// CU is 2 waves per SIMD, where the register-resident butterfly rate is 393 G/s against
+// 430 G/s at the 4 waves the library's pass keeps (tests/native/ubench_bfly --occ,
+// profiles/r06_ubench_bfly_occupancy.txt): no headroom left for the overlap to win.
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(1))) void glob_void_t;
+template <bool DIT>
+__global__ __launch_bounds__(512) void k_ntt8_pipe(Ntt8Args a) {
+  extern __shared__ felt lds[];
+  constexpr uint32_t NT = 512, K = 9, E = 4096, LOGNT = 9;
+  const uint32_t B = a.batches, items = a.items, tid = threadIdx.x;
+  // LDS-DMA of item `it` into buf: instruction i of wave w fills slots [(8i + w) * 64, +64);
+  // slot s = P(q) * 8 + (gg ^ (q & 7)) (k_ntt8's rows-of-8 lidx, P(q) = q ^ ((q2 ^ q3) & 1),
+  // an involution), so lane L loads the element whose slot is its own
+  auto prefetch = [&](uint32_t it, felt* buf) {
+    const uint32_t bidx = it % B, tile = it / B;
+    const felt* src = a.src + (uint64_t)(bidx / a.src_div) * a.src_stride;
+    const uint32_t g0 = tile << 3, hi0 = g0 >> a.lo, l0 = g0 & ((1u << a.lo) - 1);
+    const uint32_t w = tid >> 6, L = tid & 63;
+#pragma unroll
+    for (uint32_t i = 0; i < 8; i++) {
+      const uint32_t s0 = (8 * i + w) * 64, sl = s0 + L, r = sl >> 3, c = sl & 7;
+      const uint32_t q = r ^ (((r >> 2) ^ (r >> 3)) & 1u), gg = c ^ (q & 7u);
+      const uint32_t ad = (hi0 << (a.lo + K)) + (q << a.lo) + l0 + gg;
+      __builtin_amdgcn_global_load_lds((glob_void_t*)(src + ad), (lds_void_t*)(buf + s0), 16, 0, 0);
+    }
+  };
+  uint32_t it = blockIdx.x;
+  if (it < items) prefetch(it, lds);
+  for (uint32_t k = 0; it < items; it += gridDim.x, k ^= 1) {
+    felt* cur = lds + k * E;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this tile's DMA (and the last tile's stores)
+    lds_barrier();  // every wave's DMA landed; every wave is past the other buffer's last reads
+    if (it + gridDim.x < items) prefetch(it + gridDim.x, lds + (k ^ 1) * E);
+    ntt8_tile<DIT, NT, K, false, true>(a, it % B, it / B, cur);
+  }
+  (void)LOGNT;
 }
 
 }  // namespace
@@ -562,6 +632,9 @@ static void launch_ntt_radix2(Prof& prof, hipStream_t s, const NttBatch& b, uint
 // radix-8 register-blocked passes: 256-thread blocks (E = 2048 elements, K <= 8)
 // for the big transforms (several blocks per CU overlap load and compute);
 // n must be >= 2^11.
+#ifndef ZKP_NTT_PIPE
+#define ZKP_NTT_PIPE 0  // tuning builds set 1 (k_ntt8_pipe for the 9-stage direct-load passes)
+#endif
 #ifndef ZKP_NTT_ONE_PASS_MAX
 #define ZKP_NTT_ONE_PASS_MAX 11  // (tuning builds set 13: see one_pass in launch_ntt)
 #endif
@@ -569,6 +642,9 @@ static void launch_ntt_radix2(Prof& prof, hipStream_t s, const NttBatch& b, uint
 uint32_t ntt_passes(uint32_t logn) {
   if (logn < 11 || logn <= ZKP_NTT_ONE_PASS_MAX) return 1;
   if (logn == 19 || logn == 20) return 2;
+#ifdef ZKP_NTT_PLAN22
+  if (logn == 21 || logn == 22) return 2;
+#endif
 #ifdef ZKP_NTT_KFIRST
   if (logn >= 12 && logn <= 16 && logn - ZKP_NTT_KFIRST >= 5 && logn - ZKP_NTT_KFIRST <= 9) return 2;
 #endif
@@ -592,7 +668,13 @@ void launch_ntt(Prof& prof, hipStream_t s, const NttBatch& b, uint32_t logn, boo
   // as before (3+3+3+2 | 3+3(+3)) and a third less HBM traffic than 6+6+8
   // (tests/native/kbench_ntt.cpp: with the butterflies compiled out the 6+6+8 passes
   // take 1.13 of the 1.65 ms of a 48-array 2^20 LDE, about three copies of the data).
-  const bool two11 = logn == 19 || logn == 20;
+  // Round 6: 2^17-2^18 as 11 + 6/7 too (instead of 9 + 8/9 in 512-thread blocks): the 11-stage
+  // pass runs 5 waves per SIMD against the 9-stage pass's 4 (tests/native/kbench_ntt 18: the
+  // 48-array LDE 0.368 -> 0.352 ms, the DIF 0.065 -> 0.057; profiles/r06_ab_ntt_11_7_2e18.txt)
+#ifndef ZKP_NTT_TWO11_LOW
+#define ZKP_NTT_TWO11_LOW 1  // tuning builds set 0: the 9 + 8/9 plan
+#endif
+  const bool two11 = logn == 19 || logn == 20 || (ZKP_NTT_TWO11_LOW && (logn == 17 || logn == 18));
   // 2^11: the whole transform in one 11-stage pass (one array per 256-thread block, rows
   // of 1 felt): one HBM read and write per array instead of 6 + 5 stages' two.
   // (2^13 in one 1024-thread pass — 128 KB of LDS, one block per CU — was slower than
@@ -636,6 +718,15 @@ void launch_ntt(Prof& prof, hipStream_t s, const NttBatch& b, uint32_t logn, boo
     for (const void* f : k9) (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 4096 * 16);
     const void* k12[] = {(const void*)k_ntt8<true, 512, 12, true>, (const void*)k_ntt8<false, 512, 12, true>};
     for (const void* f : k12) (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 4096 * 16);
+#ifdef ZKP_NTT_PLAN22
+    const void* k10[] = {(const void*)k_ntt8<true, 512, 10, false>, (const void*)k_ntt8<false, 512, 10, false>,
+                         (const void*)k_ntt8<true, 512, 10, true>, (const void*)k_ntt8<false, 512, 10, true>};
+    for (const void* f : k10) (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 4096 * 16);
+#endif
+#if ZKP_NTT_PIPE
+    const void* kp[] = {(const void*)k_ntt8_pipe<true>, (const void*)k_ntt8_pipe<false>};
+    for (const void* f : kp) (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 2 * 4096 * 16);
+#endif
     const void* k13[] = {(const void*)k_ntt8<true, 1024, 13, true>, (const void*)k_ntt8<false, 1024, 13, true>};
     for (const void* f : k13) (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 8192 * 16);
     attr_devs |= 1ull << (dev & 63);
@@ -643,6 +734,14 @@ void launch_ntt(Prof& prof, hipStream_t s, const NttBatch& b, uint32_t logn, boo
   }
   // pass sizes: prefer multiples of 3 (whole radix-8 rounds), largest pass last
   uint32_t Ks[4] = {0, 0, 0, 0};
+#ifdef ZKP_NTT_PLAN22  // tuning builds only (tests/native kbench22): 2^21-2^22 in two passes, 12 + 9/10 or 11 + 10/11
+  if (logn == 21 || logn == 22) {
+    npass = 2;
+    const uint32_t k0 = ZKP_NTT_PLAN22 == 1210 ? 12 : 11;  // the lo = 0 pass
+    Ks[0] = dit ? k0 : logn - k0;
+    Ks[1] = dit ? logn - k0 : k0;
+  } else
+#endif
 #ifdef ZKP_NTT_KFIRST  // tuning builds only (tests/native kbench13): the lo = 0 pass takes KFIRST stages
   if (!one_pass && !two11 && logn >= 12 && logn <= 16 && logn - ZKP_NTT_KFIRST >= 5 && logn - ZKP_NTT_KFIRST <= 9) {
     npass = 2;
@@ -680,7 +779,8 @@ void launch_ntt(Prof& prof, hipStream_t s, const NttBatch& b, uint32_t logn, boo
     // (2^19-2^20 with < 8 arrays, e.g. a sharded rank's 2-column interpolation rounds beside
     // its LDE: the 64-KB blocks wait for LDS next to the other stream's kernels — C5 rank
     // ntt_dif 0.75 -> 2.04 ms, profiles/r05_ab_rank_c5_ntt9.txt — so those keep 256 threads)
-    const uint32_t lognt = one_pass ? logn - 3 : K == 9 && (!two11 || b.batches >= 8) ? 9 : 8, loge = lognt + 3;
+    const uint32_t lognt = one_pass ? logn - 3 : (K == 12 || K == 10) ? 9 : K == 9 && (!two11 || b.batches >= 8) ? 9 : 8,
+                   loge = lognt + 3;
     Ntt8Args a;
     bool first = p == 0;
     a.src = first ? b.src : b.dst;
@@ -723,6 +823,21 @@ void launch_ntt(Prof& prof, hipStream_t s, const NttBatch& b, uint32_t logn, boo
     const double bytes = arr * ((double)src_arrays + scale_rows + b.batches);
     // the pass over stages 0..2 (lo = 0): the trivial-twiddle variant
     const bool small = a.lo == 0;
+    a.batches = b.batches;
+    a.items = grid.x * grid.y;
+#if ZKP_NTT_PIPE
+    // the 9-stage direct-load pass in rows of 8, software-pipelined (k_ntt8_pipe): one
+    // persistent block per CU
+    if (K == 9 && lognt == 9 && !a.scale && a.logT == 3 && a.logTl == 3 && !a.tile_major) {
+      static int cus = 0;
+      if (!cus) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+      const uint32_t blocks = std::min<uint32_t>(a.items, cus > 0 ? (uint32_t)cus : 256u);
+      LAUNCH(prof, dit ? "ntt_dit" : "ntt_dif", s, bytes,
+             if (dit) hipLaunchKernelGGL(k_ntt8_pipe<true>, dim3(blocks), dim3(512), 2 * shmem, s, a);
+             else hipLaunchKernelGGL(k_ntt8_pipe<false>, dim3(blocks), dim3(512), 2 * shmem, s, a));
+      continue;
+    }
+#endif
 #define ZKP_NTT8(D, NTT, KK)                                                                                   \
   LAUNCH(prof, D ? "ntt_dit" : "ntt_dif", s, bytes,                                                           \
          if (small) hipLaunchKernelGGL((k_ntt8<D, NTT, KK, true>), grid, dim3(NTT), shmem, s, a);              \
@@ -738,10 +853,17 @@ void launch_ntt(Prof& prof, hipStream_t s, const NttBatch& b, uint32_t logn, boo
       case 16: ZKP_NTT8(false, 256, 8); break;
       case 19: if (lognt == 8) ZKP_NTT8(true, 256, 9); else ZKP_NTT8(true, 512, 9); break;
       case 18: if (lognt == 8) ZKP_NTT8(false, 256, 9); else ZKP_NTT8(false, 512, 9); break;
+#ifdef ZKP_NTT_PLAN22
+      case 21: ZKP_NTT8(true, 512, 10); break;
+      case 20: ZKP_NTT8(false, 512, 10); break;
+      case 23: ZKP_NTT8(true, 256, 11); break;
+      case 22: ZKP_NTT8(false, 256, 11); break;
+#else
       case 23: if (!small) launch_fail(ZKP_ERR_DEVICE, "internal: 11-stage NTT pass off lo = 0");
                ZKP_NTT8(true, 256, 11); break;
       case 22: if (!small) launch_fail(ZKP_ERR_DEVICE, "internal: 11-stage NTT pass off lo = 0");
                ZKP_NTT8(false, 256, 11); break;
+#endif
       case 25: if (!small) launch_fail(ZKP_ERR_DEVICE, "internal: 12-stage NTT pass off lo = 0");
                LAUNCH(prof, "ntt_dit", s, bytes,
                       hipLaunchKernelGGL((k_ntt8<true, 512, 12, true>), grid, dim3(512), shmem, s, a)); break;
