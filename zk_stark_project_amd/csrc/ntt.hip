@@ -643,7 +643,7 @@ uint32_t ntt_passes(uint32_t logn) {
   if (logn < 11 || logn <= ZKP_NTT_ONE_PASS_MAX) return 1;
   if (logn == 19 || logn == 20) return 2;
 #ifdef ZKP_NTT_PLAN22
-  if (logn == 21 || logn == 22) return 2;
+  if (logn == 21 || logn == 22) return ZKP_NTT_PLAN22 == 1165 ? 3 : 2;
 #endif
 #ifdef ZKP_NTT_KFIRST
   if (logn >= 12 && logn <= 16 && logn - ZKP_NTT_KFIRST >= 5 && logn - ZKP_NTT_KFIRST <= 9) return 2;
@@ -735,7 +735,13 @@ void launch_ntt(Prof& prof, hipStream_t s, const NttBatch& b, uint32_t logn, boo
   // pass sizes: prefer multiples of 3 (whole radix-8 rounds), largest pass last
   uint32_t Ks[4] = {0, 0, 0, 0};
 #ifdef ZKP_NTT_PLAN22  // tuning builds only (tests/native kbench22): 2^21-2^22 in two passes, 12 + 9/10 or 11 + 10/11
-  if (logn == 21 || logn == 22) {
+  if ((logn == 21 || logn == 22) && ZKP_NTT_PLAN22 == 1165) {  // 11 + 6 + 5/4
+    npass = 3;
+    const uint32_t k1 = 6, k2 = logn - 17;
+    Ks[0] = dit ? 11 : k2;
+    Ks[1] = k1;
+    Ks[2] = dit ? k2 : 11;
+  } else if (logn == 21 || logn == 22) {
     npass = 2;
     const uint32_t k0 = ZKP_NTT_PLAN22 == 1210 ? 12 : 11;  // the lo = 0 pass
     Ks[0] = dit ? k0 : logn - k0;
