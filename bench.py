@@ -955,6 +955,9 @@ def reference_flow_leg(device: int, check: bool) -> dict:
         "launches_per_proof": sum(v["launches"] for v in tu_kern.values()) / ntu,
         "by_kernel": {k: {"launches": v["launches"] / ntu, "ms": round(v["ms"] / ntu, 4)}
                       for k, v in sorted(tu_kern.items(), key=lambda kv: -kv[1]["ms"])},
+        # the prover's host-side stage clock (wall ms per proof, the device work inside included)
+        "host_stages_ms": {k[len("host_"):]: round(v["ms"] / ntu, 4) for k, v in sorted(tu_stats.items())
+                           if k.startswith("host_") and not k.startswith("host_ctx_")},
         "bytes_per_proof_8d": tu_bytes,
         "whole_proof_frac": round(tu_bytes / (tu_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
         "whole_proof_frac_note": "SURVEY.md §8(d)/Appendix C bytes of one TrainingUpdate proof / its warm wall ms "

@@ -215,3 +215,17 @@ def test_global_update_c5_oracle_bytes(rank_ctxs):
     assert bytes(res[0][1].trace_root) == bytes(tr.trace_root), "C5 trace root differs from the oracle"
     assert bytes(res[0][1].constraint_root) == bytes(tr.constraint_root), "C5 constraint root differs"
     check_all_equal(res, ref)
+
+
+def test_rank_emulation_small(ctx):
+    """bench.emulate_rank (the default bench line's `rank_emulation`): one rank of an 8-rank
+    proof over the loopback transport at a small MiMC shape — its device-busy time (union of
+    kernel intervals, never above their sum), launches, exchange volume and collectives."""
+    import bench
+    wl = bench.make_workload("mimc", True, 14, 8, 0, ctx)
+    r = bench.emulate_rank(ctx, wl, 8, 0, 1)
+    assert r["world"] == 8 and r["launches_per_proof"] > 20 and r["collectives_per_proof"] > 10
+    assert 0 < r["device_busy_ms_per_proof"] <= r["kernel_event_sum_ms_per_proof"] + 1e-3
+    assert r["exchange_MiB_in_per_proof"] > 0
+    w1 = bench.emulate_rank(ctx, wl, 1, 0, 1)
+    assert w1["status"] == "ok" and w1["collectives_per_proof"] == 0

@@ -5,6 +5,7 @@ barriers and the max-over-ranks reduction of the wall time (DESIGN.md §Multi-GP
 """
 from __future__ import annotations
 
+import gc
 import time
 
 
@@ -22,14 +23,22 @@ def timed_replicas(prove_once, steps: int, warmup: int, dist=None, device_sync=N
         dist.barrier()
     if device_sync is not None:
         device_sync()
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        t1 = time.perf_counter()
-        result = prove_once()
-        if times is not None:
-            times.append(time.perf_counter() - t1)
-    if device_sync is not None:
-        device_sync()
+    # no Python garbage collection inside the timed region (the steps allocate only
+    # their proof bytes; a collection pass would land in one step's time)
+    gc_was_on = gc.isenabled()
+    gc.disable()
+    try:
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            t1 = time.perf_counter()
+            result = prove_once()
+            if times is not None:
+                times.append(time.perf_counter() - t1)
+        if device_sync is not None:
+            device_sync()
+    finally:
+        if gc_was_on:
+            gc.enable()
     if dist is not None:
         dist.barrier()
     local = time.perf_counter() - t0
