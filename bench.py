@@ -69,7 +69,7 @@ KERNEL_STAGES = {
     "eval_mimc": ("eval",), "eval_linear": ("eval",),
 }
 UBENCH_BFLY = "profiles/r04_ubench_bfly.json"  # tests/native/ubench_bfly.hip on the box: the butterfly floor
-PMC_TAGS = ("r05", "r04", "r03", "r02_final", "r02", "r01")  # newest committed PMC summaries first (scripts/profile_round.sh)
+PMC_TAGS = ("r06", "r05", "r04", "r03", "r02_final", "r02", "r01")  # newest committed PMC summaries first (scripts/profile_round.sh)
 
 
 def stage_bytes(w: int, n: int, B: int, ce: int, C: int, rem: int = 7, F: int = 16) -> dict:

@@ -9,7 +9,8 @@ own streams), and their average duration, to set beside the bench line's live
   python scripts/judged_kernel_summary.py <run_kernel_trace.csv> [bench json line file]
 C2 ntt_dit = its two passes: k_ntt8<true, 256, 11, ...> dispatches with 512 position blocks
 (2^20 / 2048) and k_ntt8<true, 512, 9, ...> with 256 (2^20 / 4096);
-C3 ntt_dit = k_ntt8<true, 512, 9, ...> dispatches with 64 position blocks (2^18 / 4096)."""
+C3 ntt_dit (round 6: 11 + 7 passes at 2^18) = k_ntt8<true, 256, 11, ...> dispatches with 128 position
+blocks (2^18 / 2048) and k_ntt8<true, 256, 7, ...> with 128 (2^18 / (16 groups x 128))."""
 import csv
 import json
 import sys
@@ -21,8 +22,8 @@ def main():
     k = "void (anonymous namespace)::k_ntt8<"
     fam = {"c2_ntt_dit": lambda r: (r["Kernel_Name"].startswith(k + "true, 256, 11,") and int(r["Grid_Size_Y"]) == 512)
            or (r["Kernel_Name"].startswith(k + "true, 512, 9,") and int(r["Grid_Size_Y"]) == 256),
-           "c3_ntt_dit": lambda r: r["Kernel_Name"].startswith("void (anonymous namespace)::k_ntt8<true, 512, 9,")
-           and int(r["Grid_Size_Y"]) == 64}
+           "c3_ntt_dit": lambda r: (r["Kernel_Name"].startswith(k + "true, 256, 11,")
+                                    or r["Kernel_Name"].startswith(k + "true, 256, 7,")) and int(r["Grid_Size_Y"]) == 128}
     out = {}
     for name, pred in fam.items():
         sel = sorted((r for r in rows if pred(r)), key=lambda r: int(r["Start_Timestamp"]))

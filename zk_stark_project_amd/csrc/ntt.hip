@@ -716,6 +716,9 @@ void launch_ntt(Prof& prof, hipStream_t s, const NttBatch& b, uint32_t logn, boo
     const void* k9[] = {(const void*)k_ntt8<true, 512, 9, false>,  (const void*)k_ntt8<false, 512, 9, false>,
                         (const void*)k_ntt8<true, 512, 9, true>,   (const void*)k_ntt8<false, 512, 9, true>};
     for (const void* f : k9) (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 4096 * 16);
+    const void* k7[] = {(const void*)k_ntt8<true, 512, 7, false>, (const void*)k_ntt8<false, 512, 7, false>,
+                        (const void*)k_ntt8<true, 512, 7, true>, (const void*)k_ntt8<false, 512, 7, true>};
+    for (const void* f : k7) (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 4096 * 16);
     const void* k12[] = {(const void*)k_ntt8<true, 512, 12, true>, (const void*)k_ntt8<false, 512, 12, true>};
     for (const void* f : k12) (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 4096 * 16);
 #ifdef ZKP_NTT_PLAN22
@@ -785,7 +788,19 @@ void launch_ntt(Prof& prof, hipStream_t s, const NttBatch& b, uint32_t logn, boo
     // (2^19-2^20 with < 8 arrays, e.g. a sharded rank's 2-column interpolation rounds beside
     // its LDE: the 64-KB blocks wait for LDS next to the other stream's kernels — C5 rank
     // ntt_dif 0.75 -> 2.04 ms, profiles/r05_ab_rank_c5_ntt9.txt — so those keep 256 threads)
-    const uint32_t lognt = one_pass ? logn - 3 : (K == 12 || K == 10) ? 9 : K == 9 && (!two11 || b.batches >= 8) ? 9 : 8,
+    // 7 stages beside an 11-stage pass (2^18): 512-thread blocks, rows of 32 felts (conflict-free with
+    // the rows-of-32 swizzle; in 256-thread blocks its rows of 16 conflicted on every LDS access)
+#ifdef ZKP_NTT_K7_512
+    // tuning builds: 2^18's 7-stage pass in 512-thread blocks (rows of 32, no LDS bank
+    // conflicts) -- the DIF pass measured 0.0571 -> 0.0606 ms at 2^18 x 6 arrays (half as
+    // many workgroups), DIT unchanged: profiles/r06_kbench_ntt_k7.txt
+    const bool k7_512 = K == 7 && two11 && logn == 18;
+#else
+    const bool k7_512 = false;
+#endif
+    const uint32_t lognt = one_pass ? logn - 3
+                           : (K == 12 || K == 10 || k7_512) ? 9
+                           : K == 9 && (!two11 || b.batches >= 8) ? 9 : 8,
                    loge = lognt + 3;
     Ntt8Args a;
     bool first = p == 0;
@@ -851,11 +866,11 @@ void launch_ntt(Prof& prof, hipStream_t s, const NttBatch& b, uint32_t logn, boo
     switch (K * 2 + (dit ? 1 : 0)) {
       case 11: ZKP_NTT8(true, 256, 5); break;
       case 13: ZKP_NTT8(true, 256, 6); break;
-      case 15: ZKP_NTT8(true, 256, 7); break;
+      case 15: if (lognt == 9) ZKP_NTT8(true, 512, 7); else ZKP_NTT8(true, 256, 7); break;
       case 17: ZKP_NTT8(true, 256, 8); break;
       case 10: ZKP_NTT8(false, 256, 5); break;
       case 12: ZKP_NTT8(false, 256, 6); break;
-      case 14: ZKP_NTT8(false, 256, 7); break;
+      case 14: if (lognt == 9) ZKP_NTT8(false, 512, 7); else ZKP_NTT8(false, 256, 7); break;
       case 16: ZKP_NTT8(false, 256, 8); break;
       case 19: if (lognt == 8) ZKP_NTT8(true, 256, 9); else ZKP_NTT8(true, 512, 9); break;
       case 18: if (lognt == 8) ZKP_NTT8(false, 256, 9); else ZKP_NTT8(false, 512, 9); break;
