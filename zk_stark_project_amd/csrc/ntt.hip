@@ -257,18 +257,23 @@ __device__ __forceinline__ void ntt8_tile(const Ntt8Args& a, uint32_t bidx, uint
   // every round of both directions and the staged walk are conflict-free (checked by
   // tests/native/lds_swizzle.py's T = 1 model).
   // Round 6: conflict-free in the model (tests/native/lds_swizzle.py, the `r06` layouts)
-  // for every row length but 16: rows of 8 also flip the row's bit 0 with q bits 2^3, rows
-  // of >= 32 swizzle the felt index by q bits 0-3.
+  // for every row length: rows of 8 also flip the row's bit 0 with q bits 2^3, rows of 16
+  // (DIF) flip the felt index's bit 3 with q bits 2^4, rows of >= 32 swizzle the felt index
+  // by q bits 0-3.
   auto lidx = [](uint32_t q, uint32_t x) -> uint32_t {
     if constexpr (T == 1) {
       (void)x;
       return q ^ ((q >> 3) & 7u) ^ (((q >> 6) & 1u) << 3);
     } else if constexpr (T >= 32) {
       return q * T + (x ^ (q & 15u));
-    } else if constexpr (T == 16) {
-      // (a conflict-free swizzle exists, lds_swizzle.py's lidx_r06: four parities of q
-      // bits, but its index arithmetic took the 7-stage DIF pass from 100 to 134 VGPRs)
+    } else if constexpr (T == 16 && DIT) {
       return q * T + (x ^ (q & 7u));
+    } else if constexpr (T == 16) {
+      // DIF rounds: felt bits 0-2 ^= q bits 0-2, bit 3 ^= q bit 2 ^ q bit 4 (x ^ (q & 7)
+      // conflicted on these rounds' reads). Conflict-free in the model for both directions,
+      // but the DIT passes measured 1-3% slower with it and have no conflicts without it
+      // (profiles/r06_ab_ntt_rows16_swizzle.txt).
+      return q * T + (x ^ ((q & 7u) | ((((q >> 2) ^ (q >> 4)) & 1u) << 3)));
     } else if constexpr (T == 8) {
       return (q ^ (((q >> 2) ^ (q >> 3)) & 1u)) * T + (x ^ (q & 7u));
     } else {
