@@ -793,8 +793,8 @@ void launch_ntt(Prof& prof, hipStream_t s, const NttBatch& b, uint32_t logn, boo
     // (2^19-2^20 with < 8 arrays, e.g. a sharded rank's 2-column interpolation rounds beside
     // its LDE: the 64-KB blocks wait for LDS next to the other stream's kernels — C5 rank
     // ntt_dif 0.75 -> 2.04 ms, profiles/r05_ab_rank_c5_ntt9.txt — so those keep 256 threads)
-    // 7 stages beside an 11-stage pass (2^18): 512-thread blocks, rows of 32 felts (conflict-free with
-    // the rows-of-32 swizzle; in 256-thread blocks its rows of 16 conflicted on every LDS access)
+    // 7 stages beside an 11-stage pass (2^18): 256-thread blocks, rows of 16 felts (the DIF
+    // rounds take lidx's rows-of-16 DIF swizzle)
 #ifdef ZKP_NTT_K7_512
     // tuning builds: 2^18's 7-stage pass in 512-thread blocks (rows of 32, no LDS bank
     // conflicts) -- the DIF pass measured 0.0571 -> 0.0606 ms at 2^18 x 6 arrays (half as
