@@ -141,6 +141,8 @@ int main(int argc, char** argv) {
   // composition LDE: 6 columns x 8 cosets (DIT, coset scale fused)
   NttBatch lde{src, dst, S, n, n, B, B, cols * B};
   run("DIT lde 6 cols x 8 cosets", [&] { launch_ntt(pf, st, lde, logn, true, tw, logN); }, 10);
+  run("DIT lde 6x8, first pass only", [&] { launch_ntt(pf, st, lde, logn, true, tw, logN, 0); }, 10);
+  run("DIT lde 6x8, second pass only", [&] { launch_ntt(pf, st, lde, logn, true, tw, logN, 1); }, 10);
   {
     // the same, pipelined over two streams in column chunks: pass 1 of chunk k+1 (VALU-bound)
     // beside pass 2 of chunk k (HBM-heavier)
