@@ -491,8 +491,11 @@ __device__ __forceinline__ void ntt8_tile(const Ntt8Args& a, uint32_t bidx, uint
   (void)E;
 }
 
+// The 11-stage passes are held to 5 waves per SIMD (the DIT lo = 0 pass took 97 VGPRs, one
+// over the 5-wave budget: 92 now, no spills; profiles/r06_ab_ntt_11stage_5waves.txt). The
+// 6- and 7-stage passes would spill at 5 waves (100-116 VGPRs) and keep 4.
 template <bool DIT, int NT, int KC, bool SMALL>
-__global__ __launch_bounds__(NT) void k_ntt8(Ntt8Args a) {
+__global__ __launch_bounds__(NT, (NT == 256 && KC == 11) ? 5 : 1) void k_ntt8(Ntt8Args a) {
   extern __shared__ felt lds[];
   uint32_t bidx = blockIdx.x, tile = blockIdx.y;
   if (a.tile_major) {
