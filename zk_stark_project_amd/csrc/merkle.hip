@@ -671,9 +671,16 @@ __device__ __forceinline__ void dcoin_draw_coeffs_block(const uint32_t s[8], uin
     __syncthreads();
     return;
   }
+  // a^i for i = t + k * blockDim: a^t and a^blockDim by two independent short ladders, then
+  // one product per further i (was a full ladder per i: 4 x ~16 dependent products for the
+  // reference's w + C = 241 DEEP coefficients on a 64-thread block)
   const felt a = *s_alpha;
-  for (uint32_t i = threadIdx.x; i < ncoef; i += blockDim.x)
-    out[method == ZKP_BATCHING_HORNER ? ncoef - 1 - i : i] = fp::pow_u64(a, i);
+  const felt step = fp::pow_u64(a, blockDim.x);
+  felt p = fp::pow_u64(a, threadIdx.x);
+  for (uint32_t i = threadIdx.x; i < ncoef; i += blockDim.x) {
+    out[method == ZKP_BATCHING_HORNER ? ncoef - 1 - i : i] = p;
+    p = mul(p, step);
+  }
   __syncthreads();
 }
 
